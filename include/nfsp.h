@@ -1,0 +1,147 @@
+/*
+ * nfsp.h -- C ABI of libnfsp, the MI355X (gfx950) NFSP-on-Leduc self-play engine.
+ *
+ * The reference (dantodor/Neural-Ficititious-Self-Play-in-Imperfect-Information-Games)
+ * has no FFI: its boundary is the duck-typed Python object API that main.train calls
+ * (SURVEY.md §8b).  Every entry point below replaces one of those Python methods, in
+ * batched form (n envs / n records per call); the file:line it replaces is cited.
+ * The Python host side (the package's leduc.py / agent.py / buffers.py) binds these
+ * with ctypes exactly as INTEGRATION.md shows.
+ *
+ * Conventions
+ *   - Every function returns an int status: NFSP_OK (0) or a negative NFSP_E* code;
+ *     nfsp_last_error() returns a thread-local message for the last failure.
+ *     Game-level misuse is NOT an error, mirroring the reference, which never raises:
+ *     illegal raises are remapped (leduc/newenv.py:141-145) and a step after the hand
+ *     ended only updates env.s[p] and counts a warning (leduc/newenv.py:346-348).
+ *   - Pointers named dev_* are device (HBM) pointers, e.g. torch.Tensor.data_ptr() of a
+ *     cuda tensor; everything else is host memory.  Outputs are caller-owned; the ctx
+ *     owns env state and its workspaces.
+ *   - All work is enqueued on the ctx's stream (default: the null stream; see
+ *     nfsp_set_stream) and is asynchronous unless the function says otherwise.
+ *   - A ctx is not thread-safe (the reference is single-threaded with one env shared
+ *     by both agents, agent/agent.py:28).
+ *   - Layouts: observations are float32 [n,30] (24 history bits + 2x3 card bits, values
+ *     0/1, leduc/newenv.py:53,118), action vectors float32 [n,3], rewards float32.
+ *     Network weights are float32, packed W1[30][H] | b1[H] | W2[H][3] | b2[3]
+ *     (= Keras get_weights() order, flattened), H = hidden width (config HiddenLayer).
+ */
+#ifndef NFSP_H
+#define NFSP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NFSP_OK 0
+#define NFSP_EINVAL (-1)   /* bad argument (null pointer, size, unsupported width) */
+#define NFSP_EHIP (-2)     /* a HIP runtime call failed (message has the HIP error) */
+#define NFSP_ENOMEM (-3)
+
+#define NFSP_GAME_LEDUC 0
+
+/* MLP output activation / loss (agent/agent.py:103,106,112,115) */
+#define NFSP_ACT_RELU 0        /* BR / target-BR head, Huber loss */
+#define NFSP_ACT_SOFTMAX 1     /* AR head, categorical cross-entropy */
+
+/* Reference quirks, reproduced by default (SURVEY.md §7 hard part (b)). */
+#define NFSP_QUIRK_TERMINAL_BOOTSTRAP 1u  /* `t_batch[k] is True` never holds: terminal
+                                             transitions bootstrap (agent/agent.py:227) */
+#define NFSP_QUIRK_ROW0_TARGET 2u         /* TD targets overwrite row 0 only
+                                             (agent/agent.py:240-241) */
+#define NFSP_QUIRK_ALIAS_RL 4u            /* stored (s, a) of an RL tuple are views of
+                                             env.s[p] / env.last_action[p]: every tuple of a
+                                             hand ends up with p's LAST pre-action s and a
+                                             (utils/replay_buffer.py:30-41 + newenv.py:119) */
+#define NFSP_QUIRKS_REFERENCE 7u
+
+typedef struct nfsp_ctx nfsp_ctx;
+
+/* Record columns of an M_RL (utils/replay_buffer.py:30-41) or M_SL
+ * (utils/ReservoirBuffer.py:18-28) memory; all device pointers, rows contiguous.
+ * M_SL uses s and a only (r, s2, t = NULL). */
+typedef struct nfsp_records {
+  float* s;     /* [cap, 30] */
+  float* a;     /* [cap, 3]  */
+  float* r;     /* [cap]     */
+  float* s2;    /* [cap, 30] */
+  uint8_t* t;   /* [cap]     */
+  int64_t cap;
+} nfsp_records;
+
+/* ---------------------------------------------------------------- lifecycle */
+const char* nfsp_last_error(void);
+int nfsp_version(void);
+int nfsp_device_count(int* out);
+
+/* Creates a ctx holding n_envs Leduc hands on HIP device `device`.
+ * Replaces leduc/newenv.py:14-57 (Env.__init__), batched. */
+int nfsp_create(nfsp_ctx** out, int n_envs, uint64_t seed, int game, int device);
+int nfsp_destroy(nfsp_ctx* ctx);
+/* hip_stream: a hipStream_t (e.g. torch.cuda.current_stream().cuda_stream), 0 = null stream */
+int nfsp_set_stream(nfsp_ctx* ctx, void* hip_stream);
+int nfsp_synchronize(nfsp_ctx* ctx);
+int nfsp_num_envs(const nfsp_ctx* ctx);
+
+/* ---------------------------------------------------------------- env (batched newenv API) */
+/* Stores deals (P0, P1, public rank; rank 0 = Ace is best) for the NEXT nfsp_env_reset.
+ * Test/host injection of the deck (the reference shuffles the global `random`,
+ * leduc/deck.py:42-50; the Python drop-in shuffles there and injects the result). */
+int nfsp_env_set_deal(nfsp_ctx* ctx, const uint8_t* dev_ranks /* [n,3] */);
+/* Env.reset(dealer) (leduc/newenv.py:76-114) for every env.  Deal = the pending
+ * nfsp_env_set_deal if any, else a Philox draw keyed by (seed, env, reset index). */
+int nfsp_env_reset(nfsp_ctx* ctx, const uint8_t* dev_dealer /* [n] */);
+/* Env.get_state(p) (leduc/newenv.py:116-129).  Player = dev_players[i] if non-null, else p.
+ * Any output may be NULL.  s = env.s[p] (obs recorded by p's last step), a =
+ * env.last_action[p], r = reward if terminated else 0, s2 = current obs, t = terminated. */
+int nfsp_env_get_state(nfsp_ctx* ctx, int p, const uint8_t* dev_players,
+                       float* dev_s /*[n,30]*/, float* dev_a /*[n,3]*/, float* dev_r /*[n]*/,
+                       float* dev_s2 /*[n,30]*/, uint8_t* dev_t /*[n]*/);
+/* Env.step(action, p) (leduc/newenv.py:192-349).  Envs with dev_mask[i] == 0 are left
+ * untouched (dev_mask may be NULL = all). */
+int nfsp_env_step(nfsp_ctx* ctx, const float* dev_action /*[n,3]*/, int p,
+                  const uint8_t* dev_players, const uint8_t* dev_mask);
+/* Env.round_index (leduc/newenv.py:59-61) */
+int nfsp_env_round(nfsp_ctx* ctx, uint8_t* dev_round /*[n]*/);
+/* Debug/introspection: the 64-byte per-env state (layout nfsp_device.h `Hand`). */
+int nfsp_env_export(nfsp_ctx* ctx, void* dev_out /*[n,64] bytes*/);
+
+/* ---------------------------------------------------------------- networks */
+/* model.predict(x) (agent/agent.py:126,143,219,230) for B rows; bit-identical to the
+ * oracle's fixed summation order for 0/1 inputs. */
+int nfsp_mlp_forward(nfsp_ctx* ctx, const float* dev_w, int hidden, int act,
+                     const float* dev_x /*[B,30]*/, float* dev_y /*[B,3]*/, int64_t B);
+/* model.fit(x, y, epochs, batch_size) with plain SGD (agent/agent.py:243,261): for each
+ * epoch, rows dev_perm[e*n .. e*n+n) in slices of batch_size, one SGD step per slice.
+ * act selects the loss (RELU -> Huber, SOFTMAX -> categorical cross-entropy).
+ * Weights are updated in place.  batch_size <= 64, hidden == 64. */
+int nfsp_mlp_fit(nfsp_ctx* ctx, float* dev_w, int hidden, int act,
+                 const float* dev_x /*[n,30]*/, const float* dev_t /*[n,3]*/, int n,
+                 const int32_t* dev_perm /*[epochs,n]*/, int epochs, int batch_size, float lr);
+/* The TD-target construction of update_best_response_network (agent/agent.py:219-241):
+ * target = Q_target(s); v_k = r_k + gamma * max Q_target(s2_k) (or r_k if terminal and the
+ * TERMINAL_BOOTSTRAP quirk is off); expl = mean_k max target[k] (agent/agent.py:235-238,
+ * before the overwrite); then target[row][argmax a_k] = v_k with row = 0 under
+ * ROW0_TARGET (sequential, last k wins) else k.  dev_expl: one float64. */
+int nfsp_br_targets(nfsp_ctx* ctx, const float* dev_target_w, int hidden,
+                    const float* dev_s, const float* dev_a, const float* dev_r,
+                    const float* dev_s2, const uint8_t* dev_t, int n, double gamma,
+                    unsigned quirks, float* dev_target_out /*[n,3]*/, double* dev_expl);
+
+/* ---------------------------------------------------------------- memories */
+/* ReplayBuffer.add / ReservoirBuffer.add (utils/replay_buffer.py:30-41,
+ * utils/ReservoirBuffer.py:18-28): copy n records src[i] -> dst[dev_slots[i]].  The slot
+ * policy (FIFO head, reservoir j) is the caller's; duplicate slots: last i wins. */
+int nfsp_buf_insert(nfsp_ctx* ctx, const nfsp_records* dst, const nfsp_records* src,
+                    const int64_t* dev_slots, int64_t n);
+/* sample_batch (utils/replay_buffer.py:46-59, utils/ReservoirBuffer.py:33-43): gather
+ * dst[i] = src[dev_idx[i]] for i < k (columns that are NULL in dst are skipped). */
+int nfsp_buf_sample(nfsp_ctx* ctx, const nfsp_records* src, const int64_t* dev_idx,
+                    int64_t k, const nfsp_records* dst);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NFSP_H */

@@ -1,0 +1,129 @@
+"""ctypes binding of libnfsp (include/nfsp.h).
+
+The product path is this library: every Env / Agent / buffer operation of the package
+ends in one of these entry points.  There is no CPU fallback -- if the library or a
+GPU is missing, ``lib()`` raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libnfsp.so")
+
+OK, EINVAL, EHIP, ENOMEM = 0, -1, -2, -3
+GAME_LEDUC = 0
+ACT_RELU, ACT_SOFTMAX = 0, 1
+QUIRK_TERMINAL_BOOTSTRAP, QUIRK_ROW0_TARGET, QUIRK_ALIAS_RL = 1, 2, 4
+QUIRKS_REFERENCE = 7
+
+P = C.c_void_p
+I32, I64, U32, U64, F32, F64 = C.c_int, C.c_int64, C.c_uint, C.c_uint64, C.c_float, C.c_double
+
+
+class Records(C.Structure):
+    """``nfsp_records``: device column pointers of an M_RL / M_SL table."""
+    _fields_ = [("s", P), ("a", P), ("r", P), ("s2", P), ("t", P), ("cap", I64)]
+
+
+# name -> (restype, argtypes); must list every symbol include/nfsp.h declares
+SIGNATURES = {
+    "nfsp_last_error": (C.c_char_p, []),
+    "nfsp_version": (I32, []),
+    "nfsp_device_count": (I32, [C.POINTER(I32)]),
+    "nfsp_create": (I32, [C.POINTER(P), I32, U64, I32, I32]),
+    "nfsp_destroy": (I32, [P]),
+    "nfsp_set_stream": (I32, [P, P]),
+    "nfsp_synchronize": (I32, [P]),
+    "nfsp_num_envs": (I32, [P]),
+    "nfsp_env_set_deal": (I32, [P, P]),
+    "nfsp_env_reset": (I32, [P, P]),
+    "nfsp_env_get_state": (I32, [P, I32, P, P, P, P, P, P]),
+    "nfsp_env_step": (I32, [P, P, I32, P, P]),
+    "nfsp_env_round": (I32, [P, P]),
+    "nfsp_env_export": (I32, [P, P]),
+    "nfsp_mlp_forward": (I32, [P, P, I32, I32, P, P, I64]),
+    "nfsp_mlp_fit": (I32, [P, P, I32, I32, P, P, I32, P, I32, I32, F32]),
+    "nfsp_br_targets": (I32, [P, P, I32, P, P, P, P, P, I32, F64, U32, P, P]),
+    "nfsp_buf_insert": (I32, [P, C.POINTER(Records), C.POINTER(Records), P, I64]),
+    "nfsp_buf_sample": (I32, [P, C.POINTER(Records), P, I64, C.POINTER(Records)]),
+}
+
+_LIB = None
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH):
+    """dlopen libnfsp and bind every signature (no GPU needed)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(path):
+        raise NativeError(f"libnfsp not built: {path} is missing (run __graft_entry__.build())")
+    lib = C.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = lib
+    return lib
+
+
+def lib():
+    """The library, on a machine that has a HIP device; raises otherwise (no fallback)."""
+    L = load()
+    n = I32(0)
+    rc = L.nfsp_device_count(C.byref(n))
+    if rc != OK or n.value < 1:
+        raise NativeError("libnfsp needs a HIP device (none visible): "
+                          + L.nfsp_last_error().decode())
+    return L
+
+
+def check(rc: int, what: str = ""):
+    if rc != OK:
+        raise NativeError(f"{what} failed ({rc}): {load().nfsp_last_error().decode()}")
+
+
+def ptr(t) -> P:
+    """Device pointer of a torch tensor (or None -> NULL)."""
+    return None if t is None else P(t.data_ptr())
+
+
+def stream_handle():
+    import torch
+    return P(torch.cuda.current_stream().cuda_stream)
+
+
+class Context:
+    """Owns one ``nfsp_ctx`` (n envs on the current device), bound to torch's stream."""
+
+    def __init__(self, n_envs: int, seed: int = 1234, device: int | None = None):
+        import torch
+        L = lib()
+        self.L = L
+        dev = torch.cuda.current_device() if device is None else device
+        h = P()
+        check(L.nfsp_create(C.byref(h), int(n_envs), int(seed) & (2**64 - 1), GAME_LEDUC, dev),
+              "nfsp_create")
+        self.h = h
+        self.n = int(n_envs)
+        check(L.nfsp_set_stream(h, stream_handle()), "nfsp_set_stream")
+
+    def call(self, name, *args):
+        check(getattr(self.L, name)(self.h, *args), name)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.nfsp_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

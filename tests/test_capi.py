@@ -1,0 +1,67 @@
+"""CPU checks of the C-ABI boundary: the library builds, loads, and exports exactly
+what include/nfsp.h declares (no compute calls -- no GPU here)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "nfsp.h")
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(nfsp_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_build_and_load(pkg):
+    import __graft_entry__
+    __graft_entry__.build()
+    L = pkg.native.load()
+    assert L.nfsp_version() == 1
+
+
+def test_every_declared_symbol_exported_and_bound(pkg):
+    L = pkg.native.load()
+    decl = declared_symbols()
+    assert len(decl) >= 19
+    for name in decl:
+        assert hasattr(L, name), name
+        assert name in pkg.native.SIGNATURES, f"{name} not bound in native.py"
+    assert sorted(pkg.native.SIGNATURES) == decl
+
+
+def test_exports_are_c_abi(pkg):
+    # no C++ mangling on the boundary: every nfsp_* symbol resolves by its plain name
+    so = ctypes.CDLL(pkg.native.LIB_PATH)
+    for name in declared_symbols():
+        getattr(so, name)
+
+
+def test_errors_without_gpu_are_loud(pkg):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(pkg.native.NativeError):
+        pkg.native.lib()
+    # argument validation works without a device
+    L = pkg.native.load()
+    assert L.nfsp_create(None, 1, 0, 0, 0) == pkg.native.EINVAL
+    assert b"null" in L.nfsp_last_error()
+    assert L.nfsp_env_reset(None, None) == pkg.native.EINVAL
+
+
+def test_hand_struct_layout_matches_device_header(pkg):
+    hdr = open(os.path.join(REPO, os.path.basename(pkg.native.HERE), "csrc",
+                            "nfsp_device.h")).read()
+    assert "struct alignas(16) Hand" in hdr
+    # field order in HAND_DTYPE mirrors the struct
+    fields = ["hist", "s", "warn", "la", "rew", "rank", "dealer", "rnd", "term", "raises0",
+              "raises1", "slot", "ndone", "done0", "done1", "done2", "c0", "c1", "pad"]
+    import importlib
+    le = importlib.import_module("nfsp_amd.leduc")
+    assert list(le.HAND_DTYPE.names) == fields
+    assert le.HAND_DTYPE.itemsize == 64

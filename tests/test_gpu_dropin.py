@@ -1,0 +1,114 @@
+"""GPU parity of the drop-in Env / Agent / memories (the reference's Python API on
+libnfsp) against the CPU oracle, which tests/test_oracle_golden.py pins to the
+reference itself.
+
+* buffers: the reference's buffer trace (tests/golden/buffers_trace.npz) bit for bit;
+* main.train: the same seeds drive the oracle and the drop-in; every discrete event
+  (hands, get_state / step order, players, RL/SL inserts, samples, updates, schedules,
+  stats counters) must be identical, observations bit-exact, action vectors within
+  1e-6 (the device keeps them in fp32, the reference in fp64), network-derived
+  floats within 1e-4 after thousands of SGD steps.
+"""
+import random
+
+import numpy as np
+import pytest
+
+import nfsp_oracle as orc
+from conftest import golden
+from tracefmt import (EV_AR_UPD, EV_BR_UPD, EV_GET, EV_RESET, EV_RL_ADD, EV_SL_ADD,
+                      EV_STATS, EV_STEP, Recorder)
+
+pytestmark = pytest.mark.gpu
+
+
+def test_dropin_buffers_match_reference_trace(pkg):
+    g = golden("buffers_trace.npz")
+    B = pkg.buffers
+    buf = B.ReplayBuffer(50, 7)
+    got = []
+    at = set(g["rl_at"].tolist())
+    for i in range(180):
+        s = np.full((1, 30), float(i))
+        buf.add(s, np.full((1, 1, 3), i + 0.5), float(i % 3), s + 1000.0, bool(i % 4 == 0))
+        if i in at:
+            sb, ab, rb, s2b, tb = buf.sample_batch(16)
+            got.append((sb[:, 0, 0], ab[:, 0, 0], rb, s2b[:, 0, 0], tb))
+    assert np.array_equal(np.concatenate([x[0] for x in got]), g["rl_ids"])
+    assert np.array_equal(np.concatenate([x[1] for x in got]), g["rl_a"])
+    assert np.array_equal(np.concatenate([x[2] for x in got]), g["rl_r"])
+    assert np.array_equal(np.concatenate([x[3] for x in got]), g["rl_s2"])
+    assert np.array_equal(np.concatenate([x[4] for x in got]).astype(np.uint8), g["rl_t"])
+
+    res = B.ReservoirBuffer(40, 11)
+    got = []
+    at = set(g["sl_at"].tolist())
+    for i in range(300):
+        res.add(np.full((1, 1, 30), float(i)), np.full((1, 1, 3), i * 0.25))
+        if i in at:
+            sb, ab = res.sample_batch(12)
+            got.append((sb[:, 0, 0], ab[:, 0, 0]))
+    assert np.array_equal(np.concatenate([x[0] for x in got]), g["sl_ids"])
+    assert np.array_equal(np.concatenate([x[1] for x in got]), g["sl_a"])
+    final = res.table.s[:40, 0].cpu().numpy()
+    assert np.array_equal(final, g["sl_final"])
+
+
+def test_dropin_replay_alias_semantics(pkg):
+    """Stored views keep changing until the env replaces its arrays (reference quirk)."""
+    buf = pkg.buffers.ReplayBuffer(100, 1)
+    live = np.zeros((2, 1, 30))
+    buf.add(live[0], np.zeros((1, 1, 3)) + 1, 0, np.zeros((1, 1, 30)), False)
+    live[0][0][:] = 1.0                         # env.step rewrites s[p] in place
+    sb = buf.sample_batch(1)[0]
+    assert sb.reshape(30).tolist() == [1.0] * 30
+    other = np.zeros((2, 1, 30))                # env.reset: new arrays
+    buf.add(other[0], np.zeros((1, 1, 3)) + 1, 0, np.zeros((1, 1, 30)), False)
+    live[0][0][:] = 5.0                         # the old hand's array no longer matters
+    assert buf.table.s[0, 0].item() == 1.0
+
+
+def run(make_main, train, env_cls, rb, rs, ag_cls, episodes, init_seed):
+    rec = Recorder()
+    rec.wrap_classes(env_cls, rb, rs, ag_cls)
+    try:
+        random.seed(0)
+        env, p1, p2 = make_main(init_seed=init_seed)
+        curve = train(env, p1, p2, episodes)
+    finally:
+        rec.restore()
+    code, who, pay = rec.arrays()
+    return code, who, pay, curve, (p1, p2)
+
+
+def test_dropin_main_train_matches_oracle(pkg):
+    episodes, seed = 1200, 5
+    c0, w0, p0, curve0, ag0 = run(orc.make_main, orc.train, orc.Env, orc.ReplayBuffer,
+                                  orc.ReservoirBuffer, orc.Agent, episodes, seed)
+    S = pkg.selfplay
+    c1, w1, p1, curve1, ag1 = run(S.make_main, S.train, pkg.leduc.Env, pkg.buffers.ReplayBuffer,
+                                  pkg.buffers.ReservoirBuffer, pkg.agent.Agent, episodes, seed)
+    assert len(c0) == len(c1)
+    assert np.array_equal(c0, c1)
+    assert np.array_equal(w0, w1)
+    exact = np.isin(c0, [EV_RESET, EV_RL_ADD, EV_SL_ADD])
+    assert np.array_equal(p0[exact], p1[exact])
+    g = c0 == EV_GET     # s bits, a0..a2, r, s2 bits, t
+    assert np.array_equal(p0[g][:, [0, 4, 5, 6]], p1[g][:, [0, 4, 5, 6]])
+    assert np.abs(p0[g][:, 1:4] - p1[g][:, 1:4]).max() <= 1e-6
+    st = c0 == EV_STEP
+    assert np.abs(p0[st][:, :3] - p1[st][:, :3]).max() <= 1e-6
+    assert np.array_equal(p0[st][:, 3], p1[st][:, 3])
+    br = c0 == EV_BR_UPD  # iteration, eps, lr, expl, temp
+    assert br.sum() > 10
+    assert np.array_equal(p0[br][:, [0, 1, 2, 4]], p1[br][:, [0, 1, 2, 4]])
+    assert np.abs(p0[br][:, 3] - p1[br][:, 3]).max() <= 1e-4
+    sa = c0 == EV_STATS  # played, actions, reward exact; payoff proxy within tol
+    assert np.array_equal(p0[sa][:, :5], p1[sa][:, :5])
+    assert np.abs(p0[sa][:, 5] - p1[sa][:, 5]).max() <= 1e-4
+    assert (c0 == EV_AR_UPD).sum() == (c1 == EV_AR_UPD).sum()
+    assert np.allclose(curve0, curve1, atol=2e-4)
+    for a, b in zip(ag0, ag1):
+        for m in ("avg_strategy_model", "best_response_model", "target_br_model"):
+            for x, y in zip(getattr(a, m).get_weights(), getattr(b, m).get_weights()):
+                assert np.abs(x - y).max() <= 1e-4, m
