@@ -1,0 +1,194 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Leduc NFSP self-play hands/s (BASELINE.json `metric`).
+
+One step = one pass of the hot path over one batch: every lane of the engine plays one
+hand (fused rollout kernel: deal, eta draws, D/L/D scheduler, AR / eps-greedy BR forwards,
+env transitions, RL/SL records), the records are inserted into the agents' memories,
+and the learner runs update_strategy at the REFERENCE cadence (one per 128 RL inserts
+of an agent: AR fit + BR targets/fit/schedules/target sync).  Nothing is skipped inside
+the timed region.
+
+Workload (config.workload): C3 = 1,048,576 lanes per GPU, M_RL 200k, M_SL 2M, target
+sync every 150 BR updates (BASELINE.json configs[2]; configs[3] is the same per GPU at
+N = 8).  `--config c2` selects configs[1] (65,536 lanes).
+
+Multi-GPU (`torch.distributed.run --nproc-per-node N bench.py --gpus N`): independent
+self-play replicas, one per GPU, seeds 1234 + rank, no data-path collective (weak
+scaling); a barrier and a max-over-ranks of the elapsed time bracket the timed region.
+
+Roofline: HIP events recorded on the engine's stream around every kernel launch give
+each kernel's average duration; the dominant kernel's algorithmic FLOPs (or bytes) per
+launch / that duration is `roofline.achieved`.  `cpu_baseline`: the oracle restatement
+of the reference's main.train (oracle/nfsp_oracle.py, reference cadence, numpy MLPs) on
+one host core for a bounded number of seconds.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+CONFIGS = {
+    "c3": dict(n_lanes=1_048_576, rl_capacity=200_000, sl_capacity=2_000_000,
+               label="C3: 1,048,576 Leduc lanes/GPU, device M_RL 200k + M_SL 2M, target sync 150, "
+                     "reference update cadence (1 update_strategy / 128 RL inserts / agent)"),
+    "c2": dict(n_lanes=65_536, rl_capacity=40_000, sl_capacity=40_000,
+               label="C2: 65,536 Leduc lanes/GPU, M_RL/M_SL 40k, eta 0.1, 2x64 MLP heads, "
+                     "reference update cadence"),
+}
+
+PEAK_FP32_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA peak
+PEAK_HBM_GBS = 8000.0         # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
+# algorithmic work per unit (DESIGN.md "Measurement")
+F_FWD = 2 * (30 * 64 + 64 * 3)          # 4,224 FLOP per row forward (dense-equivalent)
+F_TRAIN = 3 * F_FWD                      # forward + backward (dX, dW) per row
+BYTES_RL, BYTES_SL = 257, 132            # reference tuple layout in fp32
+
+
+def learner_flops(br_updates, ar_updates, batch=128, epochs=2):
+    br = br_updates * (2 * batch * F_FWD + epochs * batch * F_TRAIN)
+    ar = ar_updates * (epochs * batch * F_TRAIN)
+    return br + ar
+
+
+def cpu_baseline(seconds: float):
+    """The reference-structured CPU path: oracle Env/Agent + main.train's loop."""
+    import random
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import nfsp_oracle as orc
+    random.seed(0)
+    env, p1, p2 = orc.make_main(init_seed=0)
+    players = [p1, p2]
+    dealer = random.randint(0, 1)
+    hands = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for _ in range(50):
+            dealer = 1 - dealer
+            orc.play_hand(env, players, dealer, 0.1)
+            hands += 1
+    dt = time.perf_counter() - t0
+    return {"value": hands / dt, "unit": "hands/s", "cores": 1, "kind": "port",
+            "sample": f"{hands} hands of main.train restated on the CPU (oracle/nfsp_oracle.py: "
+                      f"Env, Agent play/updates at the reference cadence, numpy fp32 MLPs), "
+                      f"{dt:.1f} s on one core"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import __graft_entry__
+    pkg = __graft_entry__.load_package()
+    cfg = CONFIGS[args.config]
+    eng = pkg.engine.SelfPlayEngine(n_lanes=cfg["n_lanes"], rl_capacity=cfg["rl_capacity"],
+                                    sl_capacity=cfg["sl_capacity"], seed=1234 + rank,
+                                    init_seed=rank)
+    for _ in range(args.warmup):
+        eng.step()
+    torch.cuda.synchronize()
+    s0 = eng.stats()
+    eng.set_timing(True)
+    eng.timings()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.step()
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    timings = eng.timings()
+    s1 = eng.stats()
+
+    hands_rank = args.steps * cfg["n_lanes"]
+    value = hands_rank * world / elapsed
+    br_upd = sum(s1["br_updates"]) - sum(s0["br_updates"])
+    ar_upd = sum(s1["ar_updates"]) - sum(s0["ar_updates"])
+    rl_ins = sum(s1["rl_total"]) - sum(s0["rl_total"])
+    sl_ins = sum(s1["sl_total"]) - sum(s0["sl_total"])
+    k_ms = {k: v[0] / max(v[1], 1) for k, v in timings.items()}
+    # dominant kernel by total time in the timed region
+    dom = max(timings, key=lambda k: timings[k][0])
+    flops_learner = learner_flops(br_upd, ar_upd) / max(timings["k_learner"][1], 1)
+    t_rl, t_sl = rl_ins / hands_rank, sl_ins / hands_rank
+    bytes_hand = BYTES_RL * t_rl + BYTES_SL * t_sl
+    rollout_bytes = bytes_hand * cfg["n_lanes"]
+    roof_rollout = {"kernel": "k_rollout", "bound": "hbm",
+                    "achieved": rollout_bytes / (k_ms["k_rollout"] * 1e-3) / 1e9,
+                    "peak": PEAK_HBM_GBS, "unit": "GB/s", "traffic": None,
+                    "bytes_per_hand": bytes_hand, "avg_ms": k_ms["k_rollout"]}
+    roof_rollout["frac"] = roof_rollout["achieved"] / PEAK_HBM_GBS
+    if dom == "k_learner":
+        ach = flops_learner / (k_ms["k_learner"] * 1e-3) / 1e12
+        roofline = {"kernel": "k_learner", "bound": "mfma", "achieved": ach,
+                    "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": ach / PEAK_FP32_TFLOPS,
+                    "traffic": None, "avg_ms": k_ms["k_learner"],
+                    "flop_per_launch": flops_learner}
+    else:
+        roofline = dict(roof_rollout)
+    rollout_path_ms = k_ms["k_rollout"] + k_ms["k_scan"] + k_ms["k_commit"]
+    out = {
+        "metric": "Leduc self-play hands/sec",
+        "value": value,
+        "unit": "hands/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic: Philox self-play deals/draws, Glorot-uniform random-init nets",
+        "config": {"workload": cfg["label"], "lanes_per_gpu": cfg["n_lanes"],
+                   "rl_capacity": cfg["rl_capacity"], "sl_capacity": cfg["sl_capacity"],
+                   "inserts_per_update": 128, "batch": 128, "parallelism": f"replicas x{world}"},
+        "roofline": roofline,
+        "roofline_rollout": roof_rollout,
+        "kernel_ms": k_ms,
+        "rollout_only_hands_per_s": cfg["n_lanes"] / (rollout_path_ms * 1e-3) * world,
+        "per_step": {"br_updates": br_upd / args.steps, "ar_updates": ar_upd / args.steps,
+                     "rl_inserts_per_hand": t_rl, "sl_inserts_per_hand": t_sl},
+        "exploitability_proxy": sum(s1["exploitability"]),
+    }
+    if rank == 0 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

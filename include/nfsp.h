@@ -141,6 +141,85 @@ int nfsp_buf_insert(nfsp_ctx* ctx, const nfsp_records* dst, const nfsp_records* 
 int nfsp_buf_sample(nfsp_ctx* ctx, const nfsp_records* src, const int64_t* dev_idx,
                     int64_t k, const nfsp_records* dst);
 
+/* ---------------------------------------------------------------- batched self-play engine
+ * The fused hot path (SURVEY.md §8a rows a1-a18 at scale): n_lanes concurrent hands,
+ * one hand per lane per nfsp_rollout, both agents' memories and networks on device.
+ *
+ *   nfsp_rollout       main.train's hand loop (main.py:27-67) x n_lanes in ONE kernel:
+ *                      deal (deck.py), eta draws, D/L/D scheduler, Agent.play
+ *                      (agent/agent.py:130-156) with the AR / eps-greedy BR forwards,
+ *                      env.step; then the RL/SL records are committed in canonical
+ *                      order (lane, then play order) to the agents' memories.
+ *   nfsp_engine_update the learner for the inserts of the last rollout: update_strategy
+ *                      once per `inserts_per_update` RL inserts of an agent (the
+ *                      reference's game_step % 128 trigger), each one =
+ *                      update_avg_response_network + update_best_response_network with
+ *                      the reference schedules; M_SL inserts are applied in stream order
+ *                      between the AR updates they precede.
+ * Randomness: Philox4x32-10 keyed by cfg.seed; counters (lane, hand, draw) for the
+ * rollout and (agent, update, row) for the learner -- results do not depend on
+ * scheduling.  Deviation from the sequential reference (declared): all hands of one
+ * rollout act with the weights and epsilon at its start (policy lag <= one rollout);
+ * repeated triggers while game_step stays on a multiple of 128 are not replayed. */
+typedef struct nfsp_engine nfsp_engine;
+
+typedef struct nfsp_engine_cfg {
+  int32_t n_lanes;             /* hands in flight */
+  int32_t hidden;              /* [Agent] HiddenLayer, must be 64 */
+  int64_t rl_capacity;         /* M_RL size (reference: [Utils] Buffersize 40000) */
+  int64_t sl_capacity;         /* M_SL size (reference: 40000) */
+  int32_t batch;               /* [Agent] MiniBatchSize 128 */
+  int32_t inserts_per_update;  /* 128: game_step % 128 (agent/agent.py:153) */
+  int32_t target_every;        /* [Agent] TargetModelUpdateRate 150 */
+  int32_t epochs;              /* fit epochs, 2 (agent/agent.py:243,261) */
+  int32_t fit_batch;           /* Keras default batch_size 32 */
+  uint32_t quirks;             /* NFSP_QUIRKS_REFERENCE */
+  float eta, lr_br, lr_ar;     /* 0.1, 0.05, 0.1 */
+  double gamma, epsilon;       /* 0.95, 0.06 */
+  uint64_t seed;
+} nfsp_engine_cfg;
+
+typedef struct nfsp_engine_stats {
+  int64_t hands, rollouts;
+  int64_t rl_total[2], sl_total[2];     /* inserts ever, per agent */
+  int64_t rl_size[2], sl_size[2];       /* memory sizes (ReplayBuffer/ReservoirBuffer.size) */
+  int64_t last_rl[2], last_sl[2];       /* inserts of the last rollout */
+  int64_t br_updates[2], ar_updates[2];
+  int64_t iteration[2], target_syncs[2];
+  int64_t actions[2][3];                /* Agent.actions counters (agent/agent.py:155) */
+  double reward[2];                     /* Agent.reward */
+  double epsilon[2], temp[2], lr_br[2];
+  double exploitability[2];             /* last BR update's proxy (agent/agent.py:235-238) */
+} nfsp_engine_stats;
+
+int nfsp_engine_default_cfg(nfsp_engine_cfg* out);
+int nfsp_engine_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, nfsp_engine** out);
+int nfsp_engine_destroy(nfsp_engine* e);
+/* Device pointer to the packed weights of agent (0|1), net (0 = AR avg_strategy_model,
+ * 1 = BR best_response_model, 2 = target_br_model); read or write them in place. */
+int nfsp_engine_weights(nfsp_engine* e, int agent, int net, float** dev_w);
+int nfsp_rollout(nfsp_engine* e);
+int nfsp_engine_update(nfsp_engine* e);
+int nfsp_engine_step(nfsp_engine* e);          /* nfsp_rollout + nfsp_engine_update */
+int nfsp_engine_get_stats(nfsp_engine* e, nfsp_engine_stats* out);   /* synchronises */
+/* Views of agent's memories: M_RL is a circular log of rl_log_cap rows whose record k
+ * (k-th insert ever) sits at row k % rl_log_cap; the logical M_RL is the last
+ * min(rl_total, rl_capacity) records.  sl: the reservoir (rows [0, sl_size)).
+ * pending_sl: the last rollout's M_SL records not yet applied by nfsp_engine_update,
+ * in insert order, with rl_pos = the agent's RL insert count when each was made. */
+int nfsp_engine_memories(nfsp_engine* e, int agent, nfsp_records* rl, int64_t* rl_log_cap,
+                         nfsp_records* sl, uint32_t** dev_pending_sl_obs,
+                         float** dev_pending_sl_a, int64_t** dev_pending_sl_rl_pos);
+/* Per-kernel timing with HIP events recorded on the ctx stream around each launch:
+ * ms / launches [4] = {k_rollout, k_scan1+k_scan2, k_commit, k_learner}, accumulated since
+ * the previous nfsp_engine_get_timings (which synchronises and resets them). */
+int nfsp_engine_set_timing(nfsp_engine* e, int on);
+int nfsp_engine_get_timings(nfsp_engine* e, double* ms /*[4]*/, int64_t* launches /*[4]*/);
+/* Debug view of the last learner run: per agent and role (0 = AR, 1 = BR) the sampled
+ * rows [batch] (int64) and fit permutations [epochs][batch] (int32) of its LAST update. */
+int nfsp_engine_last_update(nfsp_engine* e, int agent, int role, int64_t** dev_rows,
+                            int32_t** dev_perms);
+
 #ifdef __cplusplus
 }
 #endif

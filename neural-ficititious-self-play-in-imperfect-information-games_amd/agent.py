@@ -183,10 +183,13 @@ class Agent:
         self.update_avg_response_network()
         self.update_best_response_network()
 
+    verbose = True      # sampled_actions prints like the reference (agent/agent.py:197)
+
     def sampled_actions(self):
-        print("{} played {} times: Folds: {}, Calls: {}, Raises: {} - Reward: {}".format(
-            self.name, self.played, self.actions[0], self.actions[1], self.actions[2],
-            self.reward))
+        if self.verbose:
+            print("{} played {} times: Folds: {}, Calls: {}, Raises: {} - Reward: {}".format(
+                self.name, self.played, self.actions[0], self.actions[1], self.actions[2],
+                self.reward))
         self.actions = np.zeros(3)
         self.played = 0
 

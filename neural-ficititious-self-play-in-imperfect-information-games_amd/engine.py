@@ -1,0 +1,169 @@
+"""Batched self-play: the fused hot path (``nfsp_engine_*`` / ``nfsp_rollout``).
+
+``SelfPlayEngine`` owns one ``nfsp_engine`` (n_lanes hands in flight, both agents'
+networks and memories in HBM).  ``step()`` = one hand per lane through the fused
+rollout kernel + the deterministic insert + the learner at the reference cadence
+(one update_strategy per ``inserts_per_update`` RL inserts of an agent,
+agent/agent.py:153).  Configuration keys mirror config.ini:
+
+    reference (config C1)   n_lanes=1,   rl_capacity=40_000,  sl_capacity=40_000
+    C2                      n_lanes=65_536
+    C3                      n_lanes=1_048_576, rl_capacity=200_000, sl_capacity=2_000_000
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import native
+
+NP = 30 * 64 + 64 + 64 * 3 + 3
+NET_AR, NET_BR, NET_TARGET = 0, 1, 2
+
+PRESETS = {
+    "reference": dict(n_lanes=1, rl_capacity=40_000, sl_capacity=40_000),
+    "c2": dict(n_lanes=65_536, rl_capacity=40_000, sl_capacity=40_000),
+    "c3": dict(n_lanes=1_048_576, rl_capacity=200_000, sl_capacity=2_000_000),
+}
+
+
+def glorot_net(rng: np.random.RandomState, hidden: int = 64) -> np.ndarray:
+    """Keras defaults: glorot_uniform kernels, zero biases; packed like nfsp.h."""
+    def g(fi, fo):
+        lim = np.sqrt(6.0 / (fi + fo))
+        return rng.uniform(-lim, lim, size=(fi, fo)).astype(np.float32)
+    return np.concatenate([g(30, hidden).ravel(), np.zeros(hidden, np.float32),
+                           g(hidden, 3).ravel(), np.zeros(3, np.float32)])
+
+
+class SelfPlayEngine:
+    def __init__(self, ctx: native.Context | None = None, init_seed: int = 0, **cfg):
+        self.ctx = ctx if ctx is not None else native.Context(1)
+        L = self.ctx.L
+        c = native.EngineCfg()
+        native.check(L.nfsp_engine_default_cfg(C.byref(c)), "nfsp_engine_default_cfg")
+        for k, v in cfg.items():
+            if not hasattr(c, k):
+                raise KeyError(k)
+            setattr(c, k, v)
+        self.cfg = c
+        h = native.P()
+        native.check(L.nfsp_engine_create(self.ctx.h, C.byref(c), C.byref(h)), "nfsp_engine_create")
+        self.h = h
+        self.L = L
+        self.dev = torch.device("cuda", torch.cuda.current_device())
+        # initial weights in the reference's construction order: per agent AR, BR, target
+        # (the target is drawn, then overwritten with BR: agent/agent.py:67-72)
+        rng = np.random.RandomState(init_seed)
+        for a in (0, 1):
+            ar = glorot_net(rng)
+            br = glorot_net(rng)
+            glorot_net(rng)
+            self.set_weights(a, NET_AR, ar)
+            self.set_weights(a, NET_BR, br)
+            self.set_weights(a, NET_TARGET, br)
+
+    # -- weights ------------------------------------------------------------------
+    def _wptr(self, agent, net):
+        p = native.P()
+        native.check(self.L.nfsp_engine_weights(self.h, agent, net, C.byref(p)), "weights")
+        return p.value
+
+    def weights_tensor(self, agent, net) -> torch.Tensor:
+        """A torch view (no copy) of the device weights of (agent, net)."""
+        return _wrap_device(self._wptr(agent, net), NP, torch.float32, self.dev)
+
+    def get_weights(self, agent, net) -> np.ndarray:
+        return self.weights_tensor(agent, net).cpu().numpy().copy()
+
+    def set_weights(self, agent, net, flat):
+        self.weights_tensor(agent, net).copy_(torch.as_tensor(np.asarray(flat, np.float32)))
+
+    # -- hot path -----------------------------------------------------------------
+    def rollout(self):
+        native.check(self.L.nfsp_rollout(self.h), "nfsp_rollout")
+
+    def update(self):
+        native.check(self.L.nfsp_engine_update(self.h), "nfsp_engine_update")
+
+    def step(self):
+        native.check(self.L.nfsp_engine_step(self.h), "nfsp_engine_step")
+
+    def stats(self) -> dict:
+        s = native.EngineStats()
+        native.check(self.L.nfsp_engine_get_stats(self.h, C.byref(s)), "nfsp_engine_get_stats")
+        return s.to_dict()
+
+    KERNELS = ("k_rollout", "k_scan", "k_commit", "k_learner")
+
+    def set_timing(self, on=True):
+        native.check(self.L.nfsp_engine_set_timing(self.h, int(bool(on))), "set_timing")
+
+    def timings(self) -> dict:
+        """{kernel: (total ms, launches)} since the last call (HIP events, ctx stream)."""
+        ms = (native.F64 * 4)()
+        n = (native.I64 * 4)()
+        native.check(self.L.nfsp_engine_get_timings(self.h, ms, n), "get_timings")
+        return {k: (ms[i], n[i]) for i, k in enumerate(self.KERNELS)}
+
+    # -- inspection (tests) -------------------------------------------------------
+    def memories(self, agent):
+        rl, sl = native.Records(), native.Records()
+        cap = native.I64()
+        px, pa, pp = native.P(), native.P(), native.P()
+        native.check(self.L.nfsp_engine_memories(self.h, agent, C.byref(rl), C.byref(cap),
+                                                  C.byref(sl), C.byref(px), C.byref(pa),
+                                                  C.byref(pp)), "nfsp_engine_memories")
+        n = cap.value
+        d = self.dev
+        out = dict(
+            log_cap=n,
+            rl_s=_wrap_device(rl.s, n * 30, torch.float32, d).view(n, 30),
+            rl_a=_wrap_device(rl.a, n * 3, torch.float32, d).view(n, 3),
+            rl_r=_wrap_device(rl.r, n, torch.float32, d),
+            rl_s2=_wrap_device(rl.s2, n * 30, torch.float32, d).view(n, 30),
+            rl_t=_wrap_device(rl.t, n, torch.uint8, d),
+            sl_s=_wrap_device(sl.s, sl.cap * 30, torch.float32, d).view(sl.cap, 30),
+            sl_a=_wrap_device(sl.a, sl.cap * 3, torch.float32, d).view(sl.cap, 3),
+        )
+        pc = 4 * self.cfg.n_lanes
+        out["pend_x"] = _wrap_device(px.value, pc, torch.int32, d)
+        out["pend_a"] = _wrap_device(pa.value, pc * 3, torch.float32, d).view(pc, 3)
+        out["pend_pos"] = _wrap_device(pp.value, pc, torch.int64, d)
+        return out
+
+    def last_update(self, agent, role):
+        rows, perms = native.P(), native.P()
+        native.check(self.L.nfsp_engine_last_update(self.h, agent, role, C.byref(rows),
+                                                     C.byref(perms)), "last_update")
+        B, E = self.cfg.batch, self.cfg.epochs
+        return (_wrap_device(rows.value, B, torch.int64, self.dev).cpu().numpy(),
+                _wrap_device(perms.value, E * B, torch.int32, self.dev).view(E, B).cpu().numpy())
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.nfsp_engine_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _wrap_device(addr, numel, dtype, device) -> torch.Tensor:
+    """Zero-copy torch view of device memory owned by libnfsp."""
+    if numel == 0:
+        return torch.empty(0, dtype=dtype, device=device)
+
+    class _Holder:
+        pass
+    h = _Holder()
+    esize = torch.empty(0, dtype=dtype).element_size()
+    h.__cuda_array_interface__ = {
+        "shape": (int(numel),), "typestr": torch.empty(0, dtype=dtype).numpy().dtype.str,
+        "data": (int(addr), False), "version": 2, "strides": (esize,)}
+    return torch.as_tensor(h, device=device)

@@ -27,6 +27,38 @@ class Records(C.Structure):
     _fields_ = [("s", P), ("a", P), ("r", P), ("s2", P), ("t", P), ("cap", I64)]
 
 
+class EngineCfg(C.Structure):
+    """``nfsp_engine_cfg``"""
+    _fields_ = [("n_lanes", C.c_int32), ("hidden", C.c_int32), ("rl_capacity", I64),
+                ("sl_capacity", I64), ("batch", C.c_int32), ("inserts_per_update", C.c_int32),
+                ("target_every", C.c_int32), ("epochs", C.c_int32), ("fit_batch", C.c_int32),
+                ("quirks", C.c_uint32), ("eta", F32), ("lr_br", F32), ("lr_ar", F32),
+                ("gamma", F64), ("epsilon", F64), ("seed", U64)]
+
+
+class EngineStats(C.Structure):
+    """``nfsp_engine_stats``"""
+    _fields_ = [("hands", I64), ("rollouts", I64), ("rl_total", I64 * 2), ("sl_total", I64 * 2),
+                ("rl_size", I64 * 2), ("sl_size", I64 * 2), ("last_rl", I64 * 2),
+                ("last_sl", I64 * 2), ("br_updates", I64 * 2), ("ar_updates", I64 * 2),
+                ("iteration", I64 * 2), ("target_syncs", I64 * 2), ("actions", (I64 * 3) * 2),
+                ("reward", F64 * 2), ("epsilon", F64 * 2), ("temp", F64 * 2), ("lr_br", F64 * 2),
+                ("exploitability", F64 * 2)]
+
+    def to_dict(self):
+        out = {}
+        for name, _ in self._fields_:
+            v = getattr(self, name)
+            if isinstance(v, (int, float)):
+                out[name] = v
+            elif name == "actions":
+                out[name] = [list(v[0]), list(v[1])]
+            else:
+                out[name] = list(v)
+        return out
+
+
+PP = C.POINTER(P)
 # name -> (restype, argtypes); must list every symbol include/nfsp.h declares
 SIGNATURES = {
     "nfsp_last_error": (C.c_char_p, []),
@@ -48,6 +80,19 @@ SIGNATURES = {
     "nfsp_br_targets": (I32, [P, P, I32, P, P, P, P, P, I32, F64, U32, P, P]),
     "nfsp_buf_insert": (I32, [P, C.POINTER(Records), C.POINTER(Records), P, I64]),
     "nfsp_buf_sample": (I32, [P, C.POINTER(Records), P, I64, C.POINTER(Records)]),
+    "nfsp_engine_default_cfg": (I32, [C.POINTER(EngineCfg)]),
+    "nfsp_engine_create": (I32, [P, C.POINTER(EngineCfg), C.POINTER(P)]),
+    "nfsp_engine_destroy": (I32, [P]),
+    "nfsp_engine_weights": (I32, [P, I32, I32, PP]),
+    "nfsp_rollout": (I32, [P]),
+    "nfsp_engine_update": (I32, [P]),
+    "nfsp_engine_step": (I32, [P]),
+    "nfsp_engine_get_stats": (I32, [P, C.POINTER(EngineStats)]),
+    "nfsp_engine_memories": (I32, [P, I32, C.POINTER(Records), C.POINTER(I64), C.POINTER(Records),
+                                   PP, PP, PP]),
+    "nfsp_engine_last_update": (I32, [P, I32, I32, PP, PP]),
+    "nfsp_engine_set_timing": (I32, [P, I32]),
+    "nfsp_engine_get_timings": (I32, [P, C.POINTER(F64), C.POINTER(I64)]),
 }
 
 _LIB = None

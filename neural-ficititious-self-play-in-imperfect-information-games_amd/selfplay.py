@@ -37,7 +37,7 @@ def play_hand(env, players, dealer, eta):
     return policy
 
 
-def train(env, player1, player2, episodes=400000, eta=0.1, stats_every=100, verbose=False):
+def train(env, player1, player2, episodes=400000, eta=0.1, stats_every=100):
     """Returns the exploitability-proxy curve main.train plots (main.py:73-75,122)."""
     players = [player1, player2]
     dealer = random.randint(0, 1)
@@ -47,16 +47,12 @@ def train(env, player1, player2, episodes=400000, eta=0.1, stats_every=100, verb
         play_hand(env, players, dealer, eta)
         if i > 150 and i % stats_every == 0:
             for pl in players:
-                if verbose:
-                    pl.sampled_actions()
-                else:
-                    pl.actions = np.zeros(3)
-                    pl.played = 0
+                pl.sampled_actions()
             curve.append(players[0].average_payoff_br() + players[1].average_payoff_br())
     return curve
 
 
-def make_main(cfg=None, init_seed=0, quirks=None):
+def make_main(cfg=None, init_seed=0, quirks=None, verbose=False):
     c = dict(CFG, **(cfg or {}))
     env = Env(c["seed"], verbose=False)
     np.random.seed(c["seed"])
@@ -64,4 +60,5 @@ def make_main(cfg=None, init_seed=0, quirks=None):
     kw = {} if quirks is None else {"quirks": quirks}
     p1 = Agent(None, env.observation_space, env.action_space, "Player0", env, c, rng, **kw)
     p2 = Agent(None, env.observation_space, env.action_space, "Player1", env, c, rng, **kw)
+    p1.verbose = p2.verbose = verbose
     return env, p1, p2

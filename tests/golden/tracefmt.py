@@ -124,6 +124,19 @@ class Recorder:
         w(rs_cls, "add", sl_add)
         w(rb_cls, "sample_batch", rl_sample)
         w(rs_cls, "sample_batch", sl_sample)
+
+        # device-side drop-ins sample through sample_device (no host arrays): record
+        # the event and its size; the content is checked by what follows it
+        def dev_sample(code):
+            def fn(orig, buf, n):
+                out = orig(buf, n)
+                R.ev(code, R.bid(buf), out.cap)
+                return out
+            return fn
+        if "sample_device" in rb_cls.__dict__:
+            w(rb_cls, "sample_device", dev_sample(EV_RL_SAMPLE))
+        if "sample_device" in rs_cls.__dict__:
+            w(rs_cls, "sample_device", dev_sample(EV_SL_SAMPLE))
         w(agent_cls, "update_best_response_network", br_upd)
         w(agent_cls, "update_avg_response_network", ar_upd)
         w(agent_cls, "sampled_actions", stats)

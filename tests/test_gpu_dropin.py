@@ -16,8 +16,8 @@ import pytest
 
 import nfsp_oracle as orc
 from conftest import golden
-from tracefmt import (EV_AR_UPD, EV_BR_UPD, EV_GET, EV_RESET, EV_RL_ADD, EV_SL_ADD,
-                      EV_STATS, EV_STEP, Recorder)
+from tracefmt import (EV_AR_UPD, EV_BR_UPD, EV_GET, EV_RESET, EV_RL_ADD, EV_RL_SAMPLE,
+                      EV_SL_ADD, EV_SL_SAMPLE, EV_STATS, EV_STEP, Recorder)
 
 pytestmark = pytest.mark.gpu
 
@@ -88,11 +88,24 @@ def test_dropin_main_train_matches_oracle(pkg):
     S = pkg.selfplay
     c1, w1, p1, curve1, ag1 = run(S.make_main, S.train, pkg.leduc.Env, pkg.buffers.ReplayBuffer,
                                   pkg.buffers.ReservoirBuffer, pkg.agent.Agent, episodes, seed)
-    assert len(c0) == len(c1)
-    assert np.array_equal(c0, c1)
+    n = min(len(c0), len(c1))
+    bad = np.nonzero((c0[:n] != c1[:n]) | (w0[:n] != w1[:n]))[0]
+    first = int(bad[0]) if bad.size else n
+    if bad.size or len(c0) != len(c1):
+        import os
+        d = os.environ.get("NFSP_DEBUG_DIR")
+        if d:
+            np.savez(os.path.join(d, "dropin_trace.npz"), c0=c0, w0=w0, p0=p0, c1=c1, w1=w1,
+                     p1=p1)
+        lo = max(0, first - 6)
+        ctx = [(int(c0[i]), int(w0[i]), p0[i].tolist(), int(c1[i]), int(w1[i]), p1[i].tolist())
+               for i in range(lo, min(n, first + 2))]
+        raise AssertionError(f"first divergence at event {first}: {ctx}")
     assert np.array_equal(w0, w1)
     exact = np.isin(c0, [EV_RESET, EV_RL_ADD, EV_SL_ADD])
     assert np.array_equal(p0[exact], p1[exact])
+    smp = np.isin(c0, [EV_RL_SAMPLE, EV_SL_SAMPLE])   # sizes (content: via what follows)
+    assert np.array_equal(p0[smp][:, 0], p1[smp][:, 0])
     g = c0 == EV_GET     # s bits, a0..a2, r, s2 bits, t
     assert np.array_equal(p0[g][:, [0, 4, 5, 6]], p1[g][:, [0, 4, 5, 6]])
     assert np.abs(p0[g][:, 1:4] - p1[g][:, 1:4]).max() <= 1e-6
