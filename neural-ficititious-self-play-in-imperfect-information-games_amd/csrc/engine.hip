@@ -17,121 +17,14 @@
 //               AR workgroup applies the reservoir inserts in stream order in between.
 #include <math.h>
 
-#include <vector>
-
-#include "nfsp_internal.h"
-#include "nn_device.h"
+#include "engine_internal.h"
 
 using nfsp::Hand;
 using nfsp::u32x4;
 namespace nn = nfsp::nn;
+using namespace nfsp::eng;
 
 namespace {
-
-constexpr int MAXREC = 6;          // records of one kind per lane per hand (<= 6 decisions)
-constexpr int W1S = 65;            // padded LDS row stride of W1: row i of lane A and row
-                                   // i' of lane B hit banks (i + j), (i' + j) mod 32
-constexpr int NET_LDS = nfsp::OBS * W1S + nn::H + nn::H * nfsp::NA + nfsp::NA;   // 2,209
-constexpr int LB1 = nfsp::OBS * W1S, LW2 = LB1 + nn::H, LB2 = LW2 + nn::H * nfsp::NA;
-constexpr int MAX_LEARN_BATCH = 128;
-
-// Philox counter word x: rollout uses the lane id (< 2^24); learner streams use 0x8?......
-constexpr uint32_t TAG_SAMPLE = 0x81000000u, TAG_PERM = 0x82000000u, TAG_RES = 0x83000000u;
-
-struct EngineDev {
-  int64_t rl_total[2], sl_total[2], sl_count[2];
-  int64_t last_rl[2], last_sl[2];
-  int64_t iteration[2], target_count[2], target_syncs[2];
-  int64_t br_updates[2], ar_updates[2];
-  int64_t hands, rollouts;
-  unsigned long long actions[2][3];
-  long long reward_half[2];
-  double epsilon[2], temp[2], expl[2];
-  float lr_br[2];
-};
-
-struct Staging {
-  uint32_t* rl_s2;     // [MAXREC][N] observation after (bits)
-  uint32_t* rl_meta;   // [MAXREC][N] r (int8 half units) | t << 8 | player << 9
-  uint32_t* rl_s;      // [MAXREC][N] s at observation time (no-alias mode)
-  float* rl_a;         // [MAXREC][3][N]
-  uint32_t* sl_x;      // [MAXREC][N]
-  float* sl_a;         // [MAXREC][3][N]
-  uint32_t* sl_meta;   // [MAXREC][N] player | lane-local RL count << 8
-  uint32_t* fin_s;     // [2][N] env.s[p] at hand end (alias mode)
-  float* fin_a;        // [2][3][N] env.last_action[p] at hand end
-  uint32_t* counts;    // [N] rl0 | rl1 << 4 | sl0 << 8 | sl1 << 12
-  unsigned long long* local;   // [N] packed 4 x 16-bit exclusive prefix within the block
-  uint4* block_sum;    // [nblk]
-  uint4* block_base;   // [nblk]
-};
-
-struct Memories {
-  // M_RL: circular logs, agent-major [2][log_cap][...]
-  float *rl_s, *rl_a, *rl_r, *rl_s2;
-  uint8_t* rl_t;
-  int64_t log_cap;
-  // M_SL: reservoirs [2][sl_cap][...]
-  float *sl_s, *sl_a;
-  int64_t sl_cap;
-  // pending SL records of the last rollout [2][4N]
-  uint32_t* pend_x;
-  float* pend_a;
-  int64_t* pend_pos;
-  int64_t pend_cap;
-  // learner debug: last update's rows / perms per (agent, role)
-  int64_t* dbg_rows;    // [4][batch]
-  int32_t* dbg_perms;   // [4][epochs][batch]
-};
-
-__device__ inline void fwd_lds(const float* __restrict__ sw, uint32_t x, int act, float y[3]) {
-#pragma clang fp contract(off)
-  int rows[9];
-  int nb = 0;
-  uint32_t b = x;
-#pragma unroll
-  for (int u = 0; u < 9; ++u) {
-    rows[u] = 0;
-    if (b) {
-      rows[u] = __builtin_ctz(b) * W1S;
-      b &= b - 1;
-      nb = u + 1;
-    }
-  }
-  float o0 = 0.f, o1 = 0.f, o2 = 0.f;
-  for (int j = 0; j < nn::H; ++j) {
-    float acc = 0.f;
-#pragma unroll
-    for (int u = 0; u < 9; ++u)
-      if (u < nb) acc = acc + sw[rows[u] + j];
-    if (b) {   // > 9 set bits: impossible for Leduc observations, kept exact anyway
-      uint32_t rest = b;
-      while (rest) {
-        const int i = __builtin_ctz(rest);
-        rest &= rest - 1;
-        acc = acc + sw[i * W1S + j];
-      }
-    }
-    float h = acc + sw[LB1 + j];
-    h = h > 0.f ? h : 0.f;
-    o0 = o0 + h * sw[LW2 + 3 * j + 0];
-    o1 = o1 + h * sw[LW2 + 3 * j + 1];
-    o2 = o2 + h * sw[LW2 + 3 * j + 2];
-  }
-  o0 = o0 + sw[LB2 + 0];
-  o1 = o1 + sw[LB2 + 1];
-  o2 = o2 + sw[LB2 + 2];
-  if (act == NFSP_ACT_RELU) {
-    y[0] = o0 > 0.f ? o0 : 0.f;
-    y[1] = o1 > 0.f ? o1 : 0.f;
-    y[2] = o2 > 0.f ? o2 : 0.f;
-  } else {
-    const float m = fmaxf(fmaxf(o0, o1), o2);
-    const float e0 = expf(o0 - m), e1 = expf(o1 - m), e2 = expf(o2 - m);
-    const float s = (e0 + e1) + e2;
-    y[0] = e0 / s; y[1] = e1 / s; y[2] = e2 / s;
-  }
-}
 
 // ---------------------------------------------------------------------------
 // k_rollout
@@ -411,261 +304,6 @@ __global__ void __launch_bounds__(256) k_commit(int N, unsigned quirks, Staging 
   }
 }
 
-// ---------------------------------------------------------------------------
-// k_learner
-// ---------------------------------------------------------------------------
-struct LearnArgs {
-  Memories M;
-  EngineDev* st;
-  float* w;                 // [2][3][NP]
-  uint32_t k0, k1;
-  int batch, per_update, target_every, epochs, fit_batch;
-  float lr_br0, lr_ar;
-  double gamma;
-  unsigned quirks;
-  int64_t rl_cap;
-};
-
-struct LearnSmem {
-  float w[nn::NP];
-  float tw[nn::NP];                         // target net (BR role)
-  float x[MAX_LEARN_BATCH][nfsp::OBS];
-  float t[MAX_LEARN_BATCH][nfsp::NA];
-  uint32_t s2b[MAX_LEARN_BATCH];
-  float a[MAX_LEARN_BATCH][nfsp::NA];
-  float r[MAX_LEARN_BATCH];
-  uint8_t term[MAX_LEARN_BATCH];
-  int64_t cand[MAX_LEARN_BATCH];
-  uint32_t key[MAX_LEARN_BATCH];
-  int perm[4][MAX_LEARN_BATCH];
-  double vmax[MAX_LEARN_BATCH];
-  int flag;
-  nn::StepScratch sc;
-};
-
-// `batch` distinct uniform rows of [lo, lo + win): parallel draw, redraw duplicates.
-__device__ void sample_rows(LearnSmem& sm, int batch, int64_t lo, int64_t win, uint32_t stream,
-                            uint32_t m_lo, uint32_t m_hi, uint32_t k0, uint32_t k1) {
-  const int b = threadIdx.x;
-  uint32_t attempt = 0;
-  bool redraw = b < batch;
-  for (;;) {
-    if (redraw) {
-      const u32x4 u = nfsp::philox4x32({stream, m_lo, m_hi, (attempt << 8) | (uint32_t)b}, k0, k1);
-      const uint64_t r64 = ((uint64_t)u.x << 32) | u.y;
-      sm.cand[b] = lo + (int64_t)(r64 % (uint64_t)win);
-      attempt++;
-    }
-    __syncthreads();
-    bool dup = false;
-    if (b < batch)
-      for (int k = 0; k < b; ++k) dup |= sm.cand[k] == sm.cand[b];
-    redraw = dup;
-    if (!__syncthreads_or(dup)) break;
-  }
-}
-
-// epochs random permutations of [0, batch): rank of a unique random key
-__device__ void draw_perms(LearnSmem& sm, int batch, int epochs, uint32_t stream, uint32_t m_lo,
-                           uint32_t m_hi, uint32_t k0, uint32_t k1) {
-  const int b = threadIdx.x;
-  for (int e = 0; e < epochs; ++e) {
-    if (b < batch) {
-      const u32x4 u = nfsp::philox4x32({stream, m_lo, m_hi, ((uint32_t)e << 8) | (uint32_t)b}, k0, k1);
-      sm.key[b] = (u.x & ~0xFFu) | (uint32_t)b;      // unique
-    }
-    __syncthreads();
-    if (b < batch) {
-      int rank = 0;
-      for (int k = 0; k < batch; ++k) rank += sm.key[k] < sm.key[b];
-      sm.perm[e][rank] = b;
-    }
-    __syncthreads();
-  }
-}
-
-__global__ void __launch_bounds__(256) k_learner(LearnArgs A) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  LearnSmem& sm = *reinterpret_cast<LearnSmem*>(smem_raw);
-  const int agent = blockIdx.x >> 1, role = blockIdx.x & 1;   // role 0 = AR, 1 = BR
-  const int tid = threadIdx.x;
-  EngineDev* st = A.st;
-  const Memories& M = A.M;
-  float* gw = A.w + (agent * 3 + (role ? 1 : 0)) * nn::NP;
-  float* gtw = A.w + (agent * 3 + 2) * nn::NP;
-  for (int i = tid; i < nn::NP; i += blockDim.x) {
-    sm.w[i] = gw[i];
-    if (role) sm.tw[i] = gtw[i];
-  }
-  const int64_t P0 = st->rl_total[agent];
-  const int64_t n_rl = st->last_rl[agent];
-  const int64_t c = A.per_update;
-  const int64_t m_first = P0 / c + 1, m_last = (P0 + n_rl) / c;
-  const int B = A.batch;
-  const int dbg = agent * 2 + role;
-  __syncthreads();
-
-  if (role == 1) {
-    // ---------------- update_best_response_network (agent/agent.py:209-253) ----------
-    int64_t iteration = st->iteration[agent], tcount = st->target_count[agent];
-    int64_t syncs = st->target_syncs[agent], nupd = st->br_updates[agent];
-    double eps = st->epsilon[agent], temp = st->temp[agent], expl = st->expl[agent];
-    float lr = st->lr_br[agent];
-    for (int64_t m = m_first; m <= m_last; ++m) {
-      const int64_t pm = m * c;
-      const int64_t win = pm < A.rl_cap ? pm : A.rl_cap;
-      if (win <= B) continue;                         // size() > minibatch_size
-      iteration += 1;
-      sample_rows(sm, B, pm - win, win, TAG_SAMPLE | (uint32_t)dbg, (uint32_t)m,
-                  (uint32_t)(m >> 32), A.k0, A.k1);
-      // gather the minibatch (rows of the agent's log)
-      for (int e = tid; e < B * 32; e += blockDim.x) {
-        const int b = e >> 5, f = e & 31;
-        const int64_t row = (int64_t)agent * M.log_cap + sm.cand[b] % M.log_cap;
-        if (f < nfsp::OBS) sm.x[b][f] = M.rl_s[row * nfsp::OBS + f];
-        else if (f == 30) sm.r[b] = M.rl_r[row];
-        else sm.term[b] = M.rl_t[row];
-      }
-      for (int e = tid; e < B * 3; e += blockDim.x)
-        sm.a[e / 3][e % 3] = M.rl_a[((int64_t)agent * M.log_cap + sm.cand[e / 3] % M.log_cap) * 3 + e % 3];
-      if (tid < B) {
-        const int64_t row = (int64_t)agent * M.log_cap + sm.cand[tid] % M.log_cap;
-        uint32_t bits = 0;
-        for (int f = 0; f < nfsp::OBS; ++f) bits |= (M.rl_s2[row * nfsp::OBS + f] != 0.f ? 1u : 0u) << f;
-        sm.s2b[tid] = bits;
-      }
-      __syncthreads();
-      // targets with the target net (agent/agent.py:219-238)
-      if (tid < B) {
-        float q[3], qn[3], xs2[nfsp::OBS];
-        for (int f = 0; f < nfsp::OBS; ++f) xs2[f] = (float)((sm.s2b[tid] >> f) & 1u);
-        nn::forward_relu_row(sm.tw, sm.x[tid], q);
-        nn::forward_relu_row(sm.tw, xs2, qn);
-        sm.t[tid][0] = q[0]; sm.t[tid][1] = q[1]; sm.t[tid][2] = q[2];
-        const float qmax = fmaxf(fmaxf(qn[0], qn[1]), qn[2]);
-        const bool terminal = !(A.quirks & NFSP_QUIRK_TERMINAL_BOOTSTRAP) && sm.term[tid];
-        sm.vmax[tid] = terminal ? (double)sm.r[tid] : (double)sm.r[tid] + A.gamma * (double)qmax;
-      }
-      __syncthreads();
-      if (tid == 0) {
-        double acc = 0.0;
-        for (int k = 0; k < B; ++k) acc += (double)fmaxf(fmaxf(sm.t[k][0], sm.t[k][1]), sm.t[k][2]);
-        expl = acc / B;
-        for (int k = 0; k < B; ++k) {
-          const int row = (A.quirks & NFSP_QUIRK_ROW0_TARGET) ? 0 : k;
-          sm.t[row][nfsp::argmax3(sm.a[k][0], sm.a[k][1], sm.a[k][2])] = (float)sm.vmax[k];
-        }
-      }
-      draw_perms(sm, B, A.epochs, TAG_PERM | (uint32_t)dbg, (uint32_t)m, (uint32_t)(m >> 32), A.k0, A.k1);
-      for (int e = 0; e < A.epochs; ++e)
-        for (int b0 = 0; b0 < B; b0 += A.fit_batch)
-          nn::sgd_step(sm.w, &sm.x[0][0], &sm.t[0][0], &sm.perm[e][b0], min(A.fit_batch, B - b0),
-                       NFSP_ACT_RELU, lr, sm.sc);
-      // schedules (agent/agent.py:245-253, 266-273)
-      iteration += 1;
-      temp = 1.0 / (1.0 + 0.02 * sqrt((double)iteration));
-      if (tcount % A.target_every == 0) {
-        for (int i = tid; i < nn::NP; i += blockDim.x) sm.tw[i] = sm.w[i];
-        syncs++;
-      }
-      tcount++;
-      lr = (float)(A.lr_br0 / (1.0 + 0.003 * sqrt((double)iteration)));
-      eps = eps / (double)iteration;
-      nupd++;
-      if (tid < B) {
-        A.M.dbg_rows[dbg * B + tid] = sm.cand[tid];
-        for (int e = 0; e < A.epochs; ++e) A.M.dbg_perms[(dbg * A.epochs + e) * B + tid] = sm.perm[e][tid];
-      }
-      __syncthreads();
-    }
-    for (int i = tid; i < nn::NP; i += blockDim.x) {
-      gw[i] = sm.w[i];
-      gtw[i] = sm.tw[i];
-    }
-    if (tid == 0) {
-      st->iteration[agent] = iteration;
-      st->target_count[agent] = tcount;
-      st->target_syncs[agent] = syncs;
-      st->br_updates[agent] = nupd;
-      st->epsilon[agent] = eps;
-      st->temp[agent] = temp;
-      st->expl[agent] = expl;
-      st->lr_br[agent] = lr;
-      st->rl_total[agent] = P0 + n_rl;
-    }
-  } else {
-    // ---------------- update_avg_response_network (agent/agent.py:255-264) ----------
-    int64_t sl_total = st->sl_total[agent], sl_count = st->sl_count[agent];
-    int64_t nupd = st->ar_updates[agent];
-    const int64_t n_sl = st->last_sl[agent];
-    const int64_t* pend_pos = M.pend_pos + (int64_t)agent * M.pend_cap;
-    const uint32_t* pend_x = M.pend_x + (int64_t)agent * M.pend_cap;
-    const float* pend_a = M.pend_a + (int64_t)agent * M.pend_cap * 3;
-    float* res_s = M.sl_s + (int64_t)agent * M.sl_cap * nfsp::OBS;
-    float* res_a = M.sl_a + (int64_t)agent * M.sl_cap * 3;
-    int64_t cur = 0;
-    // reservoir inserts (utils/ReservoirBuffer.py:18-28) in stream order; every lane
-    // computes the slot, lane f writes field f, so a later insert to the same slot lands
-    // after the earlier one in that lane's program order (no barrier needed).
-    auto apply_until = [&](int64_t limit_pos, bool all) {
-      while (cur < n_sl && (all || pend_pos[cur] <= limit_pos)) {
-        int64_t slot;
-        if (sl_count < M.sl_cap) {
-          slot = sl_count++;
-        } else {
-          const u32x4 u = nfsp::philox4x32({TAG_RES | (uint32_t)agent, (uint32_t)sl_total,
-                                            (uint32_t)(sl_total >> 32), 0u}, A.k0, A.k1);
-          const uint64_t r64 = ((uint64_t)u.x << 32) | u.y;
-          const int64_t j = 1 + (int64_t)(r64 % (uint64_t)M.sl_cap);     // randrange(1, N+1)
-          slot = j < M.sl_cap ? j : -1;
-        }
-        sl_total++;
-        if (slot >= 0) {
-          if (tid < nfsp::OBS) res_s[slot * nfsp::OBS + tid] = (float)((pend_x[cur] >> tid) & 1u);
-          else if (tid < nfsp::OBS + 3) res_a[slot * 3 + tid - nfsp::OBS] = pend_a[cur * 3 + tid - nfsp::OBS];
-        }
-        cur++;
-      }
-    };
-    for (int64_t m = m_first; m <= m_last; ++m) {
-      const int64_t pm = m * c;
-      apply_until(pm, false);
-      if (sl_count <= B) continue;
-      __threadfence_block();
-      __syncthreads();
-      sample_rows(sm, B, 0, sl_count, TAG_SAMPLE | (uint32_t)dbg, (uint32_t)m, (uint32_t)(m >> 32),
-                  A.k0, A.k1);
-      __threadfence();   // the reservoir rows just written by this block's lanes
-      __syncthreads();
-      for (int e = tid; e < B * 33; e += blockDim.x) {
-        const int b = e / 33, f = e - b * 33;
-        const int64_t row = sm.cand[b];
-        if (f < nfsp::OBS) sm.x[b][f] = res_s[row * nfsp::OBS + f];
-        else sm.t[b][f - nfsp::OBS] = res_a[row * 3 + f - nfsp::OBS];
-      }
-      __syncthreads();
-      draw_perms(sm, B, A.epochs, TAG_PERM | (uint32_t)dbg, (uint32_t)m, (uint32_t)(m >> 32), A.k0, A.k1);
-      for (int e = 0; e < A.epochs; ++e)
-        for (int b0 = 0; b0 < B; b0 += A.fit_batch)
-          nn::sgd_step(sm.w, &sm.x[0][0], &sm.t[0][0], &sm.perm[e][b0], min(A.fit_batch, B - b0),
-                       NFSP_ACT_SOFTMAX, A.lr_ar, sm.sc);
-      nupd++;
-      if (tid < B) {
-        A.M.dbg_rows[dbg * B + tid] = sm.cand[tid];
-        for (int e = 0; e < A.epochs; ++e) A.M.dbg_perms[(dbg * A.epochs + e) * B + tid] = sm.perm[e][tid];
-      }
-      __syncthreads();
-    }
-    apply_until(0, true);
-    for (int i = tid; i < nn::NP; i += blockDim.x) gw[i] = sm.w[i];
-    if (tid == 0) {
-      st->sl_total[agent] = sl_total;
-      st->sl_count[agent] = sl_count;
-      st->ar_updates[agent] = nupd;
-    }
-  }
-}
-
 __global__ void k_finish_rollout(EngineDev* st, int64_t N) {
   if (threadIdx.x == 0) {
     st->hands += N;
@@ -678,27 +316,9 @@ __global__ void k_finish_rollout(EngineDev* st, int64_t N) {
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
-struct nfsp_engine {
-  nfsp_ctx* ctx = nullptr;
-  nfsp_engine_cfg cfg{};
-  int N = 0;
-  int nblk = 0;
-  uint64_t rollouts = 0;
-  bool pending_update = false;
-  float* w = nullptr;
-  EngineDev* st = nullptr;
-  Staging S{};
-  Memories M{};
-  std::vector<void*> allocs;
-  // optional per-kernel timing: (kernel id, start, stop) event triples on the ctx stream
-  bool timing = false;
-  std::vector<hipEvent_t> pool;
-  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> marks;
-};
-
-enum { KT_ROLLOUT = 0, KT_SCAN = 1, KT_COMMIT = 2, KT_LEARNER = 3, KT_N = 4 };
-
-static hipEvent_t eng_event(nfsp_engine* e) {
+namespace nfsp {
+namespace eng {
+hipEvent_t take_event(nfsp_engine* e) {
   if (!e->pool.empty()) {
     hipEvent_t ev = e->pool.back();
     e->pool.pop_back();
@@ -708,26 +328,8 @@ static hipEvent_t eng_event(nfsp_engine* e) {
   (void)hipEventCreate(&ev);
   return ev;
 }
-
-// RAII bracket: records start/stop events around one kernel launch when timing is on
-struct KTimer {
-  nfsp_engine* e;
-  int id;
-  hipEvent_t a = nullptr, b = nullptr;
-  KTimer(nfsp_engine* e_, int id_) : e(e_), id(id_) {
-    if (e->timing) {
-      a = eng_event(e);
-      (void)hipEventRecord(a, e->ctx->stream);
-    }
-  }
-  ~KTimer() {
-    if (e->timing) {
-      b = eng_event(e);
-      (void)hipEventRecord(b, e->ctx->stream);
-      e->marks.push_back({id, {a, b}});
-    }
-  }
-};
+}  // namespace eng
+}  // namespace nfsp
 
 static int eng_alloc(nfsp_engine* e, void** p, size_t bytes) {
   hipError_t r = hipMalloc(p, bytes);
@@ -774,6 +376,8 @@ extern "C" int nfsp_engine_destroy(nfsp_engine* e) {
     e->pool.push_back(m.second.second);
   }
   for (hipEvent_t ev : e->pool) (void)hipEventDestroy(ev);
+  for (hipStream_t st : {e->s_br[0], e->s_br[1], e->s_ar})
+    if (st) (void)hipStreamDestroy(st);
   delete e;
   return NFSP_OK;
 }
@@ -782,9 +386,10 @@ extern "C" int nfsp_engine_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, nfs
   NFSP_REQUIRE(ctx && cfg && out, "null argument");
   NFSP_REQUIRE(cfg->hidden == nn::H, "only hidden == 64 is built");
   NFSP_REQUIRE(cfg->n_lanes > 0 && cfg->n_lanes < (1 << 24), "n_lanes must be in [1, 2^24)");
-  NFSP_REQUIRE(cfg->batch >= 1 && cfg->batch <= MAX_LEARN_BATCH, "batch must be in [1, 128]");
-  NFSP_REQUIRE(cfg->fit_batch >= 1 && cfg->fit_batch <= nn::MAXB, "fit_batch must be in [1, 64]");
-  NFSP_REQUIRE(cfg->epochs >= 0 && cfg->epochs <= 4, "epochs must be in [0, 4]");
+  NFSP_REQUIRE(cfg->fit_batch == CHAIN_MB, "the SGD chains are built for fit_batch == 32");
+  NFSP_REQUIRE(cfg->batch >= CHAIN_MB && cfg->batch <= MAX_BATCH && cfg->batch % CHAIN_MB == 0,
+               "batch must be 32, 64, 96 or 128");
+  NFSP_REQUIRE(cfg->epochs >= 1 && cfg->epochs <= 4, "epochs must be in [1, 4]");
   NFSP_REQUIRE(cfg->rl_capacity > cfg->batch && cfg->sl_capacity > cfg->batch,
                "capacities must exceed the batch");
   NFSP_REQUIRE(cfg->sl_capacity < (1ll << 40) && cfg->rl_capacity < (1ll << 40), "capacity too large");
@@ -828,6 +433,26 @@ extern "C" int nfsp_engine_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, nfs
   EALLOC(e->M.pend_pos, 8 * pc);
   EALLOC(e->M.dbg_rows, 8 * 4 * cfg->batch);
   EALLOC(e->M.dbg_perms, 4 * 4 * 4 * cfg->batch);
+  // learner: <= 4N RL inserts per agent per rollout -> <= 4N / c + 2 update triggers
+  LearnBufs& L = e->LB;
+  L.umax = 4 * N / cfg->inserts_per_update + 2;
+  const int64_t ub = 2 * L.umax * cfg->batch, ueb = ub * cfg->epochs;
+  EALLOC(L.br_rows, sizeof(BrRow) * ub);
+  EALLOC(L.br_perm, ueb);
+  EALLOC(L.br_expl, sizeof(double) * 2 * L.umax);
+  EALLOC(L.br_fit, sizeof(FitRow) * ueb);
+  EALLOC(L.ar_fit, sizeof(FitRow) * ueb);
+  EALLOC(L.ar_active, 2 * L.umax);
+  EALLOC(L.res_head, sizeof(unsigned long long) * sc);
+  EALLOC(L.res_next, 4 * pc);
+  EALLOC(L.res_slot, 4 * pc);
+  for (hipStream_t* st : {&e->s_br[0], &e->s_br[1], &e->s_ar}) {
+    hipError_t sr = hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+    if (sr != hipSuccess) {
+      nfsp_engine_destroy(e);
+      return nfsp::hip_fail(sr, "nfsp_engine_create: hipStreamCreate");
+    }
+  }
   EngineDev h{};
   for (int a = 0; a < 2; ++a) {
     h.epsilon[a] = cfg->epsilon;
@@ -886,40 +511,6 @@ extern "C" int nfsp_rollout(nfsp_engine* e) {
   NFSP_LAUNCHED("k_finish_rollout");
   e->rollouts++;
   e->pending_update = true;
-  return NFSP_OK;
-}
-
-extern "C" int nfsp_engine_update(nfsp_engine* e) {
-  NFSP_REQUIRE(e, "null argument");
-  if (!e->pending_update) return NFSP_OK;
-  LearnArgs A;
-  A.M = e->M;
-  A.st = e->st;
-  A.w = e->w;
-  A.k0 = (uint32_t)e->cfg.seed;
-  A.k1 = (uint32_t)(e->cfg.seed >> 32);
-  A.batch = e->cfg.batch;
-  A.per_update = e->cfg.inserts_per_update;
-  A.target_every = e->cfg.target_every;
-  A.epochs = e->cfg.epochs;
-  A.fit_batch = e->cfg.fit_batch;
-  A.lr_br0 = e->cfg.lr_br;
-  A.lr_ar = e->cfg.lr_ar;
-  A.gamma = e->cfg.gamma;
-  A.quirks = e->cfg.quirks;
-  A.rl_cap = e->cfg.rl_capacity;
-  static bool attr_set = false;
-  if (!attr_set) {
-    NFSP_HIP(hipFuncSetAttribute((const void*)k_learner, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)sizeof(LearnSmem)));
-    attr_set = true;
-  }
-  {
-    KTimer kt(e, KT_LEARNER);
-    k_learner<<<4, 256, sizeof(LearnSmem), e->ctx->stream>>>(A);
-  }
-  NFSP_LAUNCHED("k_learner");
-  e->pending_update = false;
   return NFSP_OK;
 }
 

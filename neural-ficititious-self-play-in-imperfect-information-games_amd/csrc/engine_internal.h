@@ -1,0 +1,252 @@
+// Internals shared by engine.hip (rollout, insert, lifecycle) and learner.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <utility>
+#include <vector>
+
+#include "nfsp_internal.h"
+#include "nn_device.h"
+
+namespace nfsp {
+namespace eng {
+
+constexpr int MAXREC = 6;          // records of one kind per lane per hand (<= 6 decisions)
+constexpr int W1S = 65;            // padded LDS row stride of W1 for per-lane row gathers:
+                                   // rows i, i' of two lanes hit banks (i + j), (i' + j) mod 32
+constexpr int NET_LDS = OBS * W1S + nn::H + nn::H * NA + NA;   // 2,209 floats
+constexpr int LB1 = OBS * W1S, LW2 = LB1 + nn::H, LB2 = LW2 + nn::H * NA;
+constexpr int MAX_BATCH = 128;     // learner minibatch (config MiniBatchSize)
+constexpr int CHAIN_MB = 32;       // fit minibatch of the SGD chains (Keras batch_size)
+
+// Philox counter word x: the rollout uses the lane id (< 2^24); learner streams use these
+constexpr uint32_t TAG_SAMPLE = 0x81000000u, TAG_PERM = 0x82000000u, TAG_RES = 0x83000000u;
+
+// Device-resident engine state (one per engine), read and written by the kernels.
+struct EngineDev {
+  int64_t rl_total[2], sl_total[2], sl_count[2];
+  int64_t last_rl[2], last_sl[2];
+  int64_t iteration[2], target_count[2], target_syncs[2];
+  int64_t br_updates[2], ar_updates[2];
+  int64_t hands, rollouts;
+  unsigned long long actions[2][3];
+  long long reward_half[2];
+  double epsilon[2], temp[2], expl[2];
+  float lr_br[2];
+};
+
+struct Staging {
+  uint32_t* rl_s2;     // [MAXREC][N] observation after (bits)
+  uint32_t* rl_meta;   // [MAXREC][N] r (int8 half units) | t << 8 | player << 9
+  uint32_t* rl_s;      // [MAXREC][N] s at observation time (no-alias mode)
+  float* rl_a;         // [MAXREC][3][N]
+  uint32_t* sl_x;      // [MAXREC][N]
+  float* sl_a;         // [MAXREC][3][N]
+  uint32_t* sl_meta;   // [MAXREC][N] player | lane-local RL count << 8
+  uint32_t* fin_s;     // [2][N] env.s[p] at hand end (alias mode)
+  float* fin_a;        // [2][3][N] env.last_action[p] at hand end
+  uint32_t* counts;    // [N] rl0 | rl1 << 4 | sl0 << 8 | sl1 << 12
+  unsigned long long* local;   // [N] packed 4 x 16-bit exclusive prefix within the block
+  uint4* block_sum;    // [nblk]
+  uint4* block_base;   // [nblk]
+};
+
+struct Memories {
+  // M_RL: circular logs, agent-major [2][log_cap][...] (fp32 reference layout)
+  float *rl_s, *rl_a, *rl_r, *rl_s2;
+  uint8_t* rl_t;
+  int64_t log_cap;
+  // M_SL: reservoirs [2][sl_cap][...]
+  float *sl_s, *sl_a;
+  int64_t sl_cap;
+  // pending SL records of the last rollout [2][pend_cap], insert order
+  uint32_t* pend_x;
+  float* pend_a;
+  int64_t* pend_pos;
+  int64_t pend_cap;
+  // learner debug: last update's rows / perms per (agent, role)
+  int64_t* dbg_rows;    // [4][batch]
+  int32_t* dbg_perms;   // [4][epochs][batch]
+};
+
+// One prepared minibatch row of an SGD chain: observation bits + 3 fit targets.
+struct __attribute__((aligned(16))) FitRow {
+  uint32_t x;
+  float t0, t1, t2;
+};
+
+// A sampled M_RL row before its TD target exists.
+struct BrRow {
+  uint32_t s, s2;
+  uint32_t meta;       // argmax(a) | t << 8 | (r half units & 0xFF) << 16
+};
+
+struct LearnBufs {
+  int64_t umax;        // triggers per agent per rollout, upper bound
+  BrRow* br_rows;      // [2][umax][batch]
+  uint8_t* br_perm;    // [2][umax][epochs][batch]
+  double* br_expl;     // [2][umax]
+  FitRow* br_fit;      // [2][umax][epochs][batch]
+  FitRow* ar_fit;      // [2][umax][epochs][batch]
+  uint8_t* ar_active;  // [2][umax]
+  unsigned long long* res_head;   // [2][sl_cap]  (tag << 32 | q)
+  int32_t* res_next;   // [2][pend_cap]
+  int32_t* res_slot;   // [2][pend_cap]
+};
+
+enum { KT_ROLLOUT = 0, KT_SCAN = 1, KT_COMMIT = 2, KT_LEARNER = 3, KT_N = 4 };
+
+// Stage packed weights (W1[30][64] | b1 | W2 | b2) into the padded LDS layout of fwd_lds.
+__device__ inline void stage_net_lds(float* sw, const float* __restrict__ w, int tid, int nt) {
+  for (int q = tid; q < nn::NP; q += nt) {
+    const int d = q < nn::OB1 ? (q / nn::H) * W1S + (q % nn::H) : LB1 + (q - nn::OB1);
+    sw[d] = w[q];
+  }
+}
+
+// Forward of one 0/1 observation (bits) through a net staged by stage_net_lds.  Same
+// operation order as oracle/nn_oracle.py (bit-exact for the ReLU head).
+__device__ inline void fwd_lds(const float* __restrict__ sw, uint32_t x, int act, float y[3]) {
+#pragma clang fp contract(off)
+  int rows[9];
+  int nb = 0;
+  uint32_t b = x;
+#pragma unroll
+  for (int u = 0; u < 9; ++u) {
+    rows[u] = 0;
+    if (b) {
+      rows[u] = __builtin_ctz(b) * W1S;
+      b &= b - 1;
+      nb = u + 1;
+    }
+  }
+  float o0 = 0.f, o1 = 0.f, o2 = 0.f;
+  for (int j = 0; j < nn::H; ++j) {
+    float acc = 0.f;
+#pragma unroll
+    for (int u = 0; u < 9; ++u)
+      if (u < nb) acc = acc + sw[rows[u] + j];
+    if (b) {   // > 9 set bits: impossible for Leduc observations, kept exact anyway
+      uint32_t rest = b;
+      while (rest) {
+        const int i = __builtin_ctz(rest);
+        rest &= rest - 1;
+        acc = acc + sw[i * W1S + j];
+      }
+    }
+    float h = acc + sw[LB1 + j];
+    h = h > 0.f ? h : 0.f;
+    o0 = o0 + h * sw[LW2 + 3 * j + 0];
+    o1 = o1 + h * sw[LW2 + 3 * j + 1];
+    o2 = o2 + h * sw[LW2 + 3 * j + 2];
+  }
+  o0 = o0 + sw[LB2 + 0];
+  o1 = o1 + sw[LB2 + 1];
+  o2 = o2 + sw[LB2 + 2];
+  if (act == NFSP_ACT_RELU) {
+    y[0] = o0 > 0.f ? o0 : 0.f;
+    y[1] = o1 > 0.f ? o1 : 0.f;
+    y[2] = o2 > 0.f ? o2 : 0.f;
+  } else {
+    const float m = fmaxf(fmaxf(o0, o1), o2);
+    const float e0 = expf(o0 - m), e1 = expf(o1 - m), e2 = expf(o2 - m);
+    const float s = (e0 + e1) + e2;
+    y[0] = e0 / s; y[1] = e1 / s; y[2] = e2 / s;
+  }
+}
+
+}  // namespace eng
+}  // namespace nfsp
+
+struct nfsp_engine {
+  nfsp_ctx* ctx = nullptr;
+  nfsp_engine_cfg cfg{};
+  int N = 0;
+  int nblk = 0;
+  uint64_t rollouts = 0;
+  uint32_t learn_tag = 0;
+  bool pending_update = false;
+  float* w = nullptr;
+  nfsp::eng::EngineDev* st = nullptr;
+  nfsp::eng::Staging S{};
+  nfsp::eng::Memories M{};
+  nfsp::eng::LearnBufs LB{};
+  hipStream_t s_br[2] = {nullptr, nullptr};
+  hipStream_t s_ar = nullptr;
+  std::vector<void*> allocs;
+  // optional per-kernel timing: (kernel id, start, stop) event triples on the ctx stream
+  bool timing = false;
+  std::vector<hipEvent_t> pool;
+  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> marks;
+};
+
+namespace nfsp {
+namespace eng {
+
+hipEvent_t take_event(nfsp_engine* e);
+
+// RAII bracket: records start/stop events around launches when timing is on
+struct KTimer {
+  nfsp_engine* e;
+  int id;
+  hipEvent_t a = nullptr;
+  KTimer(nfsp_engine* e_, int id_) : e(e_), id(id_) {
+    if (e->timing) {
+      a = take_event(e);
+      (void)hipEventRecord(a, e->ctx->stream);
+    }
+  }
+  ~KTimer() {
+    if (e->timing) {
+      hipEvent_t b = take_event(e);
+      (void)hipEventRecord(b, e->ctx->stream);
+      e->marks.push_back({id, {a, b}});
+    }
+  }
+};
+
+// `batch` distinct uniform draws from [lo, lo + win) into cand[] (LDS), one per thread
+// b < batch: Philox(stream, m, (attempt << 8) | b) % win, duplicates redrawn.  Whole
+// workgroup must call.
+__device__ inline void sample_distinct(int64_t* cand, int batch, int64_t lo, int64_t win,
+                                       uint32_t stream, int64_t m, uint32_t k0, uint32_t k1) {
+  const int b = threadIdx.x;
+  uint32_t attempt = 0;
+  bool redraw = b < batch;
+  for (;;) {
+    if (redraw) {
+      const u32x4 u = philox4x32({stream, (uint32_t)m, (uint32_t)(m >> 32), (attempt << 8) | (uint32_t)b},
+                                 k0, k1);
+      const uint64_t r64 = ((uint64_t)u.x << 32) | u.y;
+      cand[b] = lo + (int64_t)(r64 % (uint64_t)win);
+      attempt++;
+    }
+    __syncthreads();
+    bool dup = false;
+    if (b < batch)
+      for (int k = 0; k < b; ++k) dup |= cand[k] == cand[b];
+    redraw = dup;
+    if (!__syncthreads_or(dup)) break;
+  }
+}
+
+// Keras fit's per-epoch shuffle: perm[e][rank] = b where rank = order of a unique random
+// key (Philox(stream, m, (e << 8) | b) with b in the low byte).  Whole workgroup calls;
+// `key` is LDS scratch of `batch` words.
+__device__ inline void draw_perm(uint32_t* key, int batch, int e, uint32_t stream, int64_t m,
+                                 uint32_t k0, uint32_t k1, int& rank_out) {
+  const int b = threadIdx.x;
+  if (b < batch) {
+    const u32x4 u = philox4x32({stream, (uint32_t)m, (uint32_t)(m >> 32), ((uint32_t)e << 8) | (uint32_t)b},
+                               k0, k1);
+    key[b] = (u.x & ~0xFFu) | (uint32_t)b;
+  }
+  __syncthreads();
+  rank_out = 0;
+  if (b < batch)
+    for (int k = 0; k < batch; ++k) rank_out += key[k] < key[b];
+  __syncthreads();
+}
+
+}  // namespace eng
+}  // namespace nfsp

@@ -1,0 +1,718 @@
+// The engine's learner (nfsp_engine_update): update_strategy at the reference cadence
+// for the RL/SL inserts of the last rollout.  Reference: agent/agent.py:192-273.
+//
+// An update's inputs (sampled rows, fit permutations, reservoir contents at that moment,
+// DQN targets) do not depend on the weights being trained, except the targets on the
+// target net, which only changes every TargetModelUpdateRate BR updates.  So all of it
+// is produced by wide parallel kernels, and the only sequential work -- the SGD steps
+// themselves -- runs in one workgroup per (agent, net) with the whole net resident:
+//
+//   k_br_prep       [all BR updates]  sample 128 M_RL rows in the window the reference
+//                                     would see, gather (s, s2, argmax a, r, t), perms
+//   k_ar_slots      [all SL inserts]  reservoir slot of every insert (Philox), per-slot
+//                                     insert lists (so any past moment can be read back)
+//   k_ar_prep       [all AR updates]  M_SL size at the trigger, sample 128 slots, read the
+//                                     slot contents AS OF the trigger, perms -> fit rows
+//   k_res_apply     [all SL inserts]  final reservoir contents (last writer per slot)
+//   k_br_targets    [a segment]       Q_target forwards, TD values, proxy, row-0 quirk
+//   k_chain<BR/AR>  [1 WG per agent]  epochs x minibatch SGD, weights in LDS/registers
+// BR chains are cut into segments at target-sync points; the two agents' BR chains and
+// the AR chains run on separate streams.
+#include <math.h>
+
+#include "engine_internal.h"
+
+using nfsp::u32x4;
+namespace nn = nfsp::nn;
+using namespace nfsp::eng;
+
+namespace {
+
+struct AgentPlan {
+  int64_t P0;          // agent's RL inserts before the last rollout
+  int64_t m_first;     // first trigger index (trigger m at RL stream position m * c)
+  int64_t U;           // triggers in the last rollout
+  int64_t m_br0;       // first trigger with a BR update (position > batch)
+  int64_t U_br;
+  int64_t n_sl;        // SL records of the last rollout
+  int64_t sl_total0;   // SL inserts before the last rollout
+};
+
+struct PrepArgs {
+  Memories M;
+  LearnBufs LB;
+  EngineDev* st;
+  AgentPlan A[2];
+  int64_t c, rl_cap;
+  int B, E;
+  uint32_t k0, k1, tag;
+};
+
+__device__ inline uint32_t row_bits(const float* __restrict__ r) {
+  uint32_t b = 0;
+#pragma unroll
+  for (int f = 0; f < nfsp::OBS; ++f) b |= (r[f] != 0.f ? 1u : 0u) << f;
+  return b;
+}
+
+// ---------------------------------------------------------------------------
+// BR prep: rows of update u of agent a (agent/agent.py:217 sample_batch)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(128) k_br_prep(PrepArgs P) {
+  __shared__ int64_t cand[MAX_BATCH];
+  __shared__ uint32_t key[MAX_BATCH];
+  const int a = blockIdx.y;
+  const int64_t u = blockIdx.x;
+  const AgentPlan& pl = P.A[a];
+  if (u >= pl.U_br) return;
+  const int b = threadIdx.x;
+  const int dbg = a * 2 + 1;
+  const int64_t m = pl.m_br0 + u;
+  const int64_t pm = m * P.c;
+  const int64_t win = pm < P.rl_cap ? pm : P.rl_cap;
+  sample_distinct(cand, P.B, pm - win, win, TAG_SAMPLE | (uint32_t)dbg, m, P.k0, P.k1);
+  const int64_t slot = (int64_t)a * P.LB.umax + u;
+  if (b < P.B) {
+    const int64_t row = (int64_t)a * P.M.log_cap + cand[b] % P.M.log_cap;
+    BrRow rr;
+    rr.s = row_bits(P.M.rl_s + row * nfsp::OBS);
+    rr.s2 = row_bits(P.M.rl_s2 + row * nfsp::OBS);
+    const float* ar = P.M.rl_a + row * 3;
+    const int am = nfsp::argmax3(ar[0], ar[1], ar[2]);
+    const int rh = (int)(P.M.rl_r[row] * 2.0f);
+    rr.meta = (uint32_t)am | ((uint32_t)P.M.rl_t[row] << 8) | (((uint32_t)rh & 0xFFu) << 16);
+    P.LB.br_rows[slot * P.B + b] = rr;
+  }
+  const bool last = u == pl.U_br - 1;
+  for (int e = 0; e < P.E; ++e) {
+    int rank;
+    draw_perm(key, P.B, e, TAG_PERM | (uint32_t)dbg, m, P.k0, P.k1, rank);
+    if (b < P.B) {
+      P.LB.br_perm[(slot * P.E + e) * P.B + rank] = (uint8_t)b;
+      if (last) P.M.dbg_perms[(dbg * P.E + e) * P.B + rank] = b;
+    }
+  }
+  if (last && b < P.B) P.M.dbg_rows[dbg * P.B + b] = cand[b];
+}
+
+// ---------------------------------------------------------------------------
+// reservoir slots + per-slot insert lists (utils/ReservoirBuffer.py:18-28)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_ar_slots(PrepArgs P) {
+  const int a = blockIdx.y;
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const AgentPlan& pl = P.A[a];
+  if (q >= pl.n_sl) return;
+  const int64_t cap = P.M.sl_cap;
+  const int64_t tot = pl.sl_total0 + q;          // adds before this one
+  int64_t slot;
+  if (tot < cap) {
+    slot = tot;                                  // append while count < buffer_size
+  } else {
+    const u32x4 r = nfsp::philox4x32({TAG_RES | (uint32_t)a, (uint32_t)tot, (uint32_t)(tot >> 32), 0u},
+                                     P.k0, P.k1);
+    const uint64_t r64 = ((uint64_t)r.x << 32) | r.y;
+    const int64_t j = 1 + (int64_t)(r64 % (uint64_t)cap);        // randrange(1, N + 1)
+    slot = j < cap ? j : -1;                                     // replace iff j < N
+  }
+  const int64_t qi = (int64_t)a * P.M.pend_cap + q;
+  P.LB.res_slot[qi] = (int32_t)slot;
+  if (slot >= 0) {
+    const unsigned long long mine = ((unsigned long long)P.tag << 32) | (unsigned long long)q;
+    const unsigned long long old = atomicExch(&P.LB.res_head[(int64_t)a * cap + slot], mine);
+    P.LB.res_next[qi] = (uint32_t)(old >> 32) == P.tag ? (int32_t)(old & 0xFFFFFFFFull) : -1;
+  }
+}
+
+// latest insert of this rollout into `slot` with index < limit (-1: none)
+__device__ inline int64_t latest_insert(const LearnBufs& LB, const Memories& M, int a, int64_t slot,
+                                        int64_t limit, uint32_t tag) {
+  const unsigned long long h = LB.res_head[(int64_t)a * M.sl_cap + slot];
+  if ((uint32_t)(h >> 32) != tag) return -1;
+  int64_t best = -1;
+  int32_t q = (int32_t)(h & 0xFFFFFFFFull);
+  while (q >= 0) {
+    if (q < limit && q > best) best = q;
+    q = LB.res_next[(int64_t)a * M.pend_cap + q];
+  }
+  return best;
+}
+
+// ---------------------------------------------------------------------------
+// AR prep (agent/agent.py:259-261): M_SL as it was at the trigger
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(128) k_ar_prep(PrepArgs P) {
+  __shared__ int64_t cand[MAX_BATCH];
+  __shared__ uint32_t key[MAX_BATCH];
+  __shared__ uint32_t rx[MAX_BATCH];
+  __shared__ float ra[MAX_BATCH][3];
+  __shared__ int64_t s_nb;
+  const int a = blockIdx.y;
+  const int64_t u = blockIdx.x;
+  const AgentPlan& pl = P.A[a];
+  if (u >= pl.U) return;
+  const int b = threadIdx.x;
+  const int dbg = a * 2 + 0;
+  const int64_t m = pl.m_first + u;
+  const int64_t pm = m * P.c;
+  const int64_t slot_u = (int64_t)a * P.LB.umax + u;
+  if (b == 0) {          // SL inserts made before the trigger: pend_pos is nondecreasing
+    const int64_t* pos = P.M.pend_pos + (int64_t)a * P.M.pend_cap;
+    int64_t lo = 0, hi = pl.n_sl;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (pos[mid] <= pm) lo = mid + 1; else hi = mid;
+    }
+    s_nb = lo;
+  }
+  __syncthreads();
+  const int64_t nb = s_nb;
+  const int64_t tot = pl.sl_total0 + nb;
+  const int64_t count = tot < P.M.sl_cap ? tot : P.M.sl_cap;
+  if (count <= P.B) {                         // size() > minibatch_size fails
+    if (b == 0) P.LB.ar_active[slot_u] = 0;
+    return;
+  }
+  if (b == 0) {
+    P.LB.ar_active[slot_u] = 1;
+    atomicAdd((unsigned long long*)&P.st->ar_updates[a], 1ull);
+  }
+  sample_distinct(cand, P.B, 0, count, TAG_SAMPLE | (uint32_t)dbg, m, P.k0, P.k1);
+  if (b < P.B) {
+    const int64_t j = cand[b];
+    const int64_t q = latest_insert(P.LB, P.M, a, j, nb, P.tag);
+    if (q >= 0) {
+      const int64_t qi = (int64_t)a * P.M.pend_cap + q;
+      rx[b] = P.M.pend_x[qi];
+      ra[b][0] = P.M.pend_a[qi * 3 + 0];
+      ra[b][1] = P.M.pend_a[qi * 3 + 1];
+      ra[b][2] = P.M.pend_a[qi * 3 + 2];
+    } else {
+      const int64_t row = (int64_t)a * P.M.sl_cap + j;
+      rx[b] = row_bits(P.M.sl_s + row * nfsp::OBS);
+      ra[b][0] = P.M.sl_a[row * 3 + 0];
+      ra[b][1] = P.M.sl_a[row * 3 + 1];
+      ra[b][2] = P.M.sl_a[row * 3 + 2];
+    }
+  }
+  const bool last = u == pl.U - 1;
+  for (int e = 0; e < P.E; ++e) {
+    int rank;
+    draw_perm(key, P.B, e, TAG_PERM | (uint32_t)dbg, m, P.k0, P.k1, rank);
+    if (b < P.B) {
+      FitRow fr;
+      fr.x = rx[b];
+      fr.t0 = ra[b][0]; fr.t1 = ra[b][1]; fr.t2 = ra[b][2];
+      P.LB.ar_fit[(slot_u * P.E + e) * P.B + rank] = fr;
+      if (last) P.M.dbg_perms[(dbg * P.E + e) * P.B + rank] = b;
+    }
+  }
+  if (last && b < P.B) P.M.dbg_rows[dbg * P.B + b] = cand[b];
+}
+
+__global__ void __launch_bounds__(256) k_res_apply(PrepArgs P) {
+  const int a = blockIdx.y;
+  const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= P.A[a].n_sl) return;
+  const int64_t qi = (int64_t)a * P.M.pend_cap + q;
+  const int64_t slot = P.LB.res_slot[qi];
+  if (slot < 0) return;
+  if (latest_insert(P.LB, P.M, a, slot, P.A[a].n_sl, P.tag) != q) return;   // a later add wins
+  const uint32_t x = P.M.pend_x[qi];
+  const int64_t row = (int64_t)a * P.M.sl_cap + slot;
+#pragma unroll
+  for (int f = 0; f < nfsp::OBS; ++f) P.M.sl_s[row * nfsp::OBS + f] = (float)((x >> f) & 1u);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) P.M.sl_a[row * 3 + c] = P.M.pend_a[qi * 3 + c];
+}
+
+// ---------------------------------------------------------------------------
+// DQN targets of one BR segment (agent/agent.py:219-241), one update per workgroup
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(128) k_br_targets(LearnBufs LB, const float* __restrict__ tw, int a,
+                                                    int64_t u0, int B, int E, double gamma,
+                                                    unsigned quirks) {
+  __shared__ __attribute__((aligned(16))) float sw[NET_LDS];
+  __shared__ float q[MAX_BATCH][3];
+  __shared__ float val[MAX_BATCH];
+  __shared__ uint32_t sb[MAX_BATCH];
+  __shared__ uint8_t am[MAX_BATCH];
+  const int b = threadIdx.x;
+  stage_net_lds(sw, tw, b, blockDim.x);
+  __syncthreads();
+  const int64_t u = u0 + blockIdx.x;
+  const int64_t slot = (int64_t)a * LB.umax + u;
+  if (b < B) {
+    const BrRow rr = LB.br_rows[slot * B + b];
+    float qb[3], qn[3];
+    fwd_lds(sw, rr.s, NFSP_ACT_RELU, qb);
+    fwd_lds(sw, rr.s2, NFSP_ACT_RELU, qn);
+    q[b][0] = qb[0]; q[b][1] = qb[1]; q[b][2] = qb[2];
+    const float qmax = fmaxf(fmaxf(qn[0], qn[1]), qn[2]);
+    const float r = (float)(int8_t)((rr.meta >> 16) & 0xFFu) * 0.5f;
+    const bool terminal = !(quirks & NFSP_QUIRK_TERMINAL_BOOTSTRAP) && ((rr.meta >> 8) & 1u);
+    val[b] = (float)(terminal ? (double)r : (double)r + gamma * (double)qmax);
+    am[b] = (uint8_t)(rr.meta & 0xFFu);
+    sb[b] = rr.s;
+  }
+  __syncthreads();
+  if (b == 0) {          // exploitability proxy, before the overwrite (agent/agent.py:235-238)
+    double acc = 0.0;
+    for (int k = 0; k < B; ++k) acc += (double)fmaxf(fmaxf(q[k][0], q[k][1]), q[k][2]);
+    LB.br_expl[slot] = acc / B;
+  }
+  __syncthreads();
+  if (quirks & NFSP_QUIRK_ROW0_TARGET) {
+    if (b < 3) {         // target[0][argmax a_k] = v_k for k = 0..B-1: the last k wins
+      int last = -1;
+      for (int k = 0; k < B; ++k)
+        if (am[k] == b) last = k;
+      if (last >= 0) q[0][b] = val[last];
+    }
+  } else if (b < B) {
+    q[b][am[b]] = val[b];
+  }
+  __syncthreads();
+  if (b < B) {
+    for (int e = 0; e < E; ++e) {
+      const int k = LB.br_perm[(slot * E + e) * B + b];
+      FitRow fr;
+      fr.x = sb[k];
+      fr.t0 = q[k][0]; fr.t1 = q[k][1]; fr.t2 = q[k][2];
+      LB.br_fit[(slot * E + e) * B + b] = fr;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// SGD chain: one workgroup (4 waves) per agent runs its updates back to back.
+// Wave w owns samples 8w..8w+7 of every 32-row minibatch, lane j owns hidden unit j.
+// W1 lives once in LDS; b1, W2 (per lane) and b2 are replicated in registers of every
+// wave and updated identically.  Minibatch rows are wave-uniform (scalar registers).
+// ---------------------------------------------------------------------------
+struct ChainArgs {
+  float* w[2];                    // weights of (agent, net)
+  float* sync_to[2];              // BR: target net to copy into at the end (or null)
+  const FitRow* fit;              // [2][umax][E][B]
+  const uint8_t* active;          // AR: per-update flag (null for BR)
+  int64_t umax;
+  int64_t u0[2], u1[2];           // update range per agent
+  int agents[2];                  // blockIdx -> agent
+  int B, E;
+  int relu;                       // 1: BR (Huber), 0: AR (cross-entropy)
+  float lr_fixed;                 // AR lr
+  double lr0;                     // BR: lr_u = lr0 / (1 + 0.003 sqrt(it0 + 2u))
+  int64_t it0[2];
+};
+
+struct ChainSmem {
+  float W1[nfsp::OBS * nn::H];
+  float gW1[4][nfsp::OBS * nn::H];
+  float gW2[4][nn::H * 3];
+  float gb1[4][nn::H];
+  float gb2[4][3];
+};
+
+// sum over the 64 lanes of 24 values; afterwards lane l holds the sums of values
+// 3(l >> 3) + {0, 1, 2} (one 8-lane group per sample)
+__device__ inline void reduce24(float (&v)[24], float& s0, float& s1, float& s2) {
+  const int lane = threadIdx.x & 63;
+  float w12[12], w6[6], w3[3];
+  const bool h5 = lane & 32, h4 = lane & 16, h3 = lane & 8;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    const float keep = h5 ? v[i + 12] : v[i];
+    const float send = h5 ? v[i] : v[i + 12];
+    w12[i] = keep + __shfl_xor(send, 32, 64);
+  }
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const float keep = h4 ? w12[i + 6] : w12[i];
+    const float send = h4 ? w12[i] : w12[i + 6];
+    w6[i] = keep + __shfl_xor(send, 16, 64);
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float keep = h3 ? w6[i + 3] : w6[i];
+    const float send = h3 ? w6[i] : w6[i + 3];
+    w3[i] = keep + __shfl_xor(send, 8, 64);
+  }
+#pragma unroll
+  for (int d = 4; d >= 1; d >>= 1) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) w3[i] += __shfl_xor(w3[i], d, 64);
+  }
+  s0 = w3[0]; s1 = w3[1]; s2 = w3[2];
+}
+
+__global__ void __launch_bounds__(256) k_chain(ChainArgs C) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  ChainSmem& sm = *reinterpret_cast<ChainSmem*>(smem_raw);
+  const int a = C.agents[blockIdx.x];
+  const int tid = threadIdx.x;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int j = tid & 63;
+  float* gw = C.w[blockIdx.x];
+  for (int i = tid; i < nfsp::OBS * nn::H; i += 256) {
+    sm.W1[i] = gw[i];
+    sm.gW1[0][i] = 0.f; sm.gW1[1][i] = 0.f; sm.gW1[2][i] = 0.f; sm.gW1[3][i] = 0.f;
+  }
+  float b1 = gw[nn::OB1 + j];
+  float W2_0 = gw[nn::OW2 + 3 * j + 0], W2_1 = gw[nn::OW2 + 3 * j + 1], W2_2 = gw[nn::OW2 + 3 * j + 2];
+  float b2_0 = gw[nn::OB2 + 0], b2_1 = gw[nn::OB2 + 1], b2_2 = gw[nn::OB2 + 2];
+  __syncthreads();
+  const int nmb = C.B / CHAIN_MB;
+  const float inv3m = 1.0f / (float)(3 * CHAIN_MB);
+  const float invm = 1.0f / (float)CHAIN_MB;
+  for (int64_t u = C.u0[blockIdx.x]; u < C.u1[blockIdx.x]; ++u) {
+    const int64_t slot = (int64_t)a * C.umax + u;
+    if (C.active && !C.active[slot]) continue;
+    const float lr = C.relu ? (float)(C.lr0 / (1.0 + 0.003 * sqrt((double)(C.it0[blockIdx.x] + 2 * u))))
+                            : C.lr_fixed;
+    for (int e = 0; e < C.E; ++e) {
+      for (int s = 0; s < nmb; ++s) {
+        const FitRow* rows = C.fit + (slot * C.E + e) * C.B + s * CHAIN_MB + w * 8;
+        uint32_t xb[8];
+        float t[8][3];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          xb[r] = __builtin_amdgcn_readfirstlane(rows[r].x);
+          t[r][0] = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(rows[r].t0)));
+          t[r][1] = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(rows[r].t1)));
+          t[r][2] = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(rows[r].t2)));
+        }
+        // ---- forward
+        float z1[8];
+        float v[24];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          float acc = 0.f;
+          uint32_t bits = xb[r];
+          while (bits) {
+            const int i = __builtin_ctz(bits);
+            bits &= bits - 1;
+            acc = acc + sm.W1[i * nn::H + j];
+          }
+          z1[r] = acc + b1;
+          const float h = z1[r] > 0.f ? z1[r] : 0.f;
+          v[3 * r + 0] = h * W2_0;
+          v[3 * r + 1] = h * W2_1;
+          v[3 * r + 2] = h * W2_2;
+        }
+        float s0, s1, s2;
+        reduce24(v, s0, s1, s2);
+        // ---- loss gradient dL/dz2 (uniform per sample)
+        float d[8][3];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const float o0 = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(s0), 8 * r)) + b2_0;
+          const float o1 = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(s1), 8 * r)) + b2_1;
+          const float o2 = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(s2), 8 * r)) + b2_2;
+          const float zz[3] = {o0, o1, o2};
+          if (C.relu) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+              const float y = zz[k] > 0.f ? zz[k] : 0.f;
+              const float ee = t[r][k] - y;
+              const float g = fabsf(ee) > 1.0f ? (ee > 0.f ? 1.f : (ee < 0.f ? -1.f : 0.f)) : ee;
+              d[r][k] = zz[k] > 0.f ? (-g * inv3m) : 0.f;
+            }
+          } else {
+            const float mx = fmaxf(fmaxf(o0, o1), o2);
+            const float e0 = expf(o0 - mx), e1 = expf(o1 - mx), e2 = expf(o2 - mx);
+            const float ssum = (e0 + e1) + e2;
+            const float y[3] = {e0 / ssum, e1 / ssum, e2 / ssum};
+            const float S = (y[0] + y[1]) + y[2];
+            const float eps = 1e-7f, hi = 1.0f - 1e-7f;
+            float dp[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+              const float p = y[k] / S;
+              const float pc = fminf(fmaxf(p, eps), hi);
+              const float msk = (p >= eps && p <= hi) ? 1.f : 0.f;
+              dp[k] = (-t[r][k] / pc) * msk * invm;
+            }
+            const float dpy = (dp[0] * y[0] + dp[1] * y[1]) + dp[2] * y[2];
+            float dy[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) dy[k] = dp[k] / S - dpy / (S * S);
+            const float dyy = (dy[0] * y[0] + dy[1] * y[1]) + dy[2] * y[2];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) d[r][k] = y[k] * (dy[k] - dyy);
+          }
+        }
+        // ---- backward
+        float g2_0 = 0.f, g2_1 = 0.f, g2_2 = 0.f, gb1 = 0.f, gb2_0 = 0.f, gb2_1 = 0.f, gb2_2 = 0.f;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const float h = z1[r] > 0.f ? z1[r] : 0.f;
+          g2_0 += h * d[r][0];
+          g2_1 += h * d[r][1];
+          g2_2 += h * d[r][2];
+          gb2_0 += d[r][0];
+          gb2_1 += d[r][1];
+          gb2_2 += d[r][2];
+          const float dh = (d[r][0] * W2_0 + d[r][1] * W2_1) + d[r][2] * W2_2;
+          const float dz = z1[r] > 0.f ? dh : 0.f;
+          gb1 += dz;
+          uint32_t bits = xb[r];
+          while (bits) {
+            const int i = __builtin_ctz(bits);
+            bits &= bits - 1;
+            sm.gW1[w][i * nn::H + j] += dz;      // this lane owns column j of wave w's partial
+          }
+        }
+        sm.gW2[w][3 * j + 0] = g2_0;
+        sm.gW2[w][3 * j + 1] = g2_1;
+        sm.gW2[w][3 * j + 2] = g2_2;
+        sm.gb1[w][j] = gb1;
+        if (j == 0) {
+          sm.gb2[w][0] = gb2_0;
+          sm.gb2[w][1] = gb2_1;
+          sm.gb2[w][2] = gb2_2;
+        }
+        __syncthreads();
+        // ---- SGD update (fixed reduction order over the 4 wave partials)
+        for (int i = tid; i < nfsp::OBS * nn::H; i += 256) {
+          const float g = ((sm.gW1[0][i] + sm.gW1[1][i]) + sm.gW1[2][i]) + sm.gW1[3][i];
+          sm.W1[i] = sm.W1[i] - lr * g;
+          sm.gW1[0][i] = 0.f; sm.gW1[1][i] = 0.f; sm.gW1[2][i] = 0.f; sm.gW1[3][i] = 0.f;
+        }
+        {
+          float g0 = ((sm.gW2[0][3 * j] + sm.gW2[1][3 * j]) + sm.gW2[2][3 * j]) + sm.gW2[3][3 * j];
+          float g1 = ((sm.gW2[0][3 * j + 1] + sm.gW2[1][3 * j + 1]) + sm.gW2[2][3 * j + 1]) +
+                     sm.gW2[3][3 * j + 1];
+          float g2 = ((sm.gW2[0][3 * j + 2] + sm.gW2[1][3 * j + 2]) + sm.gW2[2][3 * j + 2]) +
+                     sm.gW2[3][3 * j + 2];
+          const float gb = ((sm.gb1[0][j] + sm.gb1[1][j]) + sm.gb1[2][j]) + sm.gb1[3][j];
+          W2_0 = W2_0 - lr * g0;
+          W2_1 = W2_1 - lr * g1;
+          W2_2 = W2_2 - lr * g2;
+          b1 = b1 - lr * gb;
+          g0 = ((sm.gb2[0][0] + sm.gb2[1][0]) + sm.gb2[2][0]) + sm.gb2[3][0];
+          g1 = ((sm.gb2[0][1] + sm.gb2[1][1]) + sm.gb2[2][1]) + sm.gb2[3][1];
+          g2 = ((sm.gb2[0][2] + sm.gb2[1][2]) + sm.gb2[2][2]) + sm.gb2[3][2];
+          b2_0 = b2_0 - lr * g0;
+          b2_1 = b2_1 - lr * g1;
+          b2_2 = b2_2 - lr * g2;
+        }
+        __syncthreads();
+      }
+    }
+  }
+  // write back (wave 0 holds the replicated small parameters)
+  float* dsts[2] = {gw, C.sync_to[blockIdx.x]};
+  for (int k = 0; k < 2; ++k) {
+    float* dst = dsts[k];
+    if (!dst) continue;
+    for (int i = tid; i < nfsp::OBS * nn::H; i += 256) dst[i] = sm.W1[i];
+    if (w == 0) {
+      dst[nn::OB1 + j] = b1;
+      dst[nn::OW2 + 3 * j + 0] = W2_0;
+      dst[nn::OW2 + 3 * j + 1] = W2_1;
+      dst[nn::OW2 + 3 * j + 2] = W2_2;
+      if (j == 0) {
+        dst[nn::OB2 + 0] = b2_0;
+        dst[nn::OB2 + 1] = b2_1;
+        dst[nn::OB2 + 2] = b2_2;
+      }
+    }
+  }
+}
+
+// schedule state after the learner (host-computed values + device-side counters)
+struct FinalArgs {
+  EngineDev* st;
+  const double* br_expl;
+  int64_t umax;
+  int64_t n_rl[2], n_sl[2], U_br[2];
+  int64_t iteration[2], tcount[2], syncs[2];
+  double eps[2], temp[2];
+  float lr[2];
+  int64_t sl_cap;
+};
+
+__global__ void k_finalize(FinalArgs F) {
+  if (threadIdx.x != 0) return;
+  for (int a = 0; a < 2; ++a) {
+    EngineDev* st = F.st;
+    st->rl_total[a] += F.n_rl[a];
+    st->sl_total[a] += F.n_sl[a];
+    st->sl_count[a] = st->sl_total[a] < F.sl_cap ? st->sl_total[a] : F.sl_cap;
+    if (F.U_br[a] > 0) {
+      st->expl[a] = F.br_expl[(int64_t)a * F.umax + F.U_br[a] - 1];
+      st->br_updates[a] += F.U_br[a];
+      st->iteration[a] = F.iteration[a];
+      st->target_count[a] = F.tcount[a];
+      st->target_syncs[a] = F.syncs[a];
+      st->epsilon[a] = F.eps[a];
+      st->temp[a] = F.temp[a];
+      st->lr_br[a] = F.lr[a];
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int nfsp_engine_update(nfsp_engine* e) {
+  NFSP_REQUIRE(e, "null argument");
+  if (!e->pending_update) return NFSP_OK;
+  e->pending_update = false;
+  hipStream_t s = e->ctx->stream;
+  const nfsp_engine_cfg& cfg = e->cfg;
+  // the trigger plan needs the rollout's insert counts: one small readback
+  EngineDev h;
+  NFSP_HIP(hipMemcpyAsync(&h, e->st, sizeof(h), hipMemcpyDeviceToHost, s));
+  NFSP_HIP(hipStreamSynchronize(s));
+  KTimer kt(e, KT_LEARNER);
+  e->learn_tag++;
+  PrepArgs P;
+  P.M = e->M;
+  P.LB = e->LB;
+  P.st = e->st;
+  P.c = cfg.inserts_per_update;
+  P.rl_cap = cfg.rl_capacity;
+  P.B = cfg.batch;
+  P.E = cfg.epochs;
+  P.k0 = (uint32_t)cfg.seed;
+  P.k1 = (uint32_t)(cfg.seed >> 32);
+  P.tag = e->learn_tag;
+  int64_t maxU = 0, maxUbr = 0, maxSL = 0;
+  for (int a = 0; a < 2; ++a) {
+    AgentPlan& pl = P.A[a];
+    pl.P0 = h.rl_total[a];
+    const int64_t n = h.last_rl[a];
+    pl.m_first = pl.P0 / P.c + 1;
+    const int64_t m_last = (pl.P0 + n) / P.c;
+    pl.U = m_last >= pl.m_first ? m_last - pl.m_first + 1 : 0;
+    // BR update iff min(p_m, cap) > batch  <=>  m * c > batch
+    pl.m_br0 = pl.m_first > cfg.batch / P.c + 1 ? pl.m_first : cfg.batch / P.c + 1;
+    pl.U_br = m_last >= pl.m_br0 ? m_last - pl.m_br0 + 1 : 0;
+    pl.n_sl = h.last_sl[a];
+    pl.sl_total0 = h.sl_total[a];
+    NFSP_REQUIRE(pl.U <= e->LB.umax, "update plan exceeds the learner buffers");
+    maxU = pl.U > maxU ? pl.U : maxU;
+    maxUbr = pl.U_br > maxUbr ? pl.U_br : maxUbr;
+    maxSL = pl.n_sl > maxSL ? pl.n_sl : maxSL;
+  }
+  // ---- parallel prep on the ctx stream
+  if (maxUbr > 0) {
+    k_br_prep<<<dim3((unsigned)maxUbr, 2), 128, 0, s>>>(P);
+    NFSP_LAUNCHED("k_br_prep");
+  }
+  if (maxSL > 0) {
+    k_ar_slots<<<dim3(nfsp_blocks(maxSL, 256), 2), 256, 0, s>>>(P);
+    NFSP_LAUNCHED("k_ar_slots");
+  }
+  if (maxU > 0) {
+    k_ar_prep<<<dim3((unsigned)maxU, 2), 128, 0, s>>>(P);
+    NFSP_LAUNCHED("k_ar_prep");
+  }
+  if (maxSL > 0) {
+    k_res_apply<<<dim3(nfsp_blocks(maxSL, 256), 2), 256, 0, s>>>(P);
+    NFSP_LAUNCHED("k_res_apply");
+  }
+  static bool attr = false;
+  if (!attr) {
+    NFSP_HIP(hipFuncSetAttribute((const void*)k_chain, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)sizeof(ChainSmem)));
+    attr = true;
+  }
+  hipEvent_t fork = take_event(e);
+  NFSP_HIP(hipEventRecord(fork, s));
+  // ---- AR chains (both agents, one launch) on their own stream
+  if (maxU > 0) {
+    NFSP_HIP(hipStreamWaitEvent(e->s_ar, fork, 0));
+    ChainArgs C{};
+    C.fit = e->LB.ar_fit;
+    C.active = e->LB.ar_active;
+    C.umax = e->LB.umax;
+    C.B = cfg.batch;
+    C.E = cfg.epochs;
+    C.relu = 0;
+    C.lr_fixed = cfg.lr_ar;
+    for (int a = 0; a < 2; ++a) {
+      C.agents[a] = a;
+      C.w[a] = e->w + (a * 3 + 0) * nn::NP;
+      C.sync_to[a] = nullptr;
+      C.u0[a] = 0;
+      C.u1[a] = P.A[a].U;
+    }
+    k_chain<<<2, 256, sizeof(ChainSmem), e->s_ar>>>(C);
+    NFSP_LAUNCHED("k_chain(AR)");
+  }
+  // ---- BR: per agent, segments between target syncs, each = targets + chain
+  FinalArgs F{};
+  F.st = e->st;
+  F.br_expl = e->LB.br_expl;
+  F.umax = e->LB.umax;
+  F.sl_cap = cfg.sl_capacity;
+  for (int a = 0; a < 2; ++a) {
+    const AgentPlan& pl = P.A[a];
+    F.n_rl[a] = h.last_rl[a];
+    F.n_sl[a] = pl.n_sl;
+    F.U_br[a] = pl.U_br;
+    hipStream_t sa = e->s_br[a];
+    NFSP_HIP(hipStreamWaitEvent(sa, fork, 0));
+    int64_t it = h.iteration[a], tc = h.target_count[a], syncs = h.target_syncs[a];
+    double eps = h.epsilon[a];
+    const int64_t it0 = it;
+    float* wbr = e->w + (a * 3 + 1) * nn::NP;
+    float* wtg = e->w + (a * 3 + 2) * nn::NP;
+    int64_t u = 0;
+    while (u < pl.U_br) {
+      // segment [u, v): ends after the first update whose target_count % every == 0
+      int64_t v = u;
+      bool sync = false;
+      while (v < pl.U_br) {
+        const bool s_here = (tc + (v - 0)) % cfg.target_every == 0;
+        ++v;
+        if (s_here) { sync = true; break; }
+      }
+      k_br_targets<<<(unsigned)(v - u), 128, 0, sa>>>(e->LB, wtg, a, u, cfg.batch, cfg.epochs,
+                                                       cfg.gamma, cfg.quirks);
+      NFSP_LAUNCHED("k_br_targets");
+      ChainArgs C{};
+      C.fit = e->LB.br_fit;
+      C.active = nullptr;
+      C.umax = e->LB.umax;
+      C.B = cfg.batch;
+      C.E = cfg.epochs;
+      C.relu = 1;
+      C.lr0 = cfg.lr_br;
+      C.agents[0] = a;
+      C.w[0] = wbr;
+      C.sync_to[0] = sync ? wtg : nullptr;
+      C.u0[0] = u;
+      C.u1[0] = v;
+      C.it0[0] = it0;
+      k_chain<<<1, 256, sizeof(ChainSmem), sa>>>(C);
+      NFSP_LAUNCHED("k_chain(BR)");
+      u = v;
+    }
+    // schedules (agent/agent.py:245-253, 266-273) in the reference's double arithmetic
+    for (int64_t k = 0; k < pl.U_br; ++k) {
+      if (tc % cfg.target_every == 0) syncs++;
+      tc++;
+      it += 2;
+      eps = eps / (double)it;
+    }
+    F.iteration[a] = it;
+    F.tcount[a] = tc;
+    F.syncs[a] = syncs;
+    F.eps[a] = eps;
+    F.temp[a] = 1.0 / (1.0 + 0.02 * sqrt((double)it));
+    F.lr[a] = (float)(cfg.lr_br / (1.0 + 0.003 * sqrt((double)it)));
+  }
+  // ---- join and publish the schedules
+  for (hipStream_t st : {e->s_ar, e->s_br[0], e->s_br[1]}) {
+    hipEvent_t j = take_event(e);
+    NFSP_HIP(hipEventRecord(j, st));
+    NFSP_HIP(hipStreamWaitEvent(s, j, 0));
+    e->pool.push_back(j);      // reusable once the wait is enqueued
+  }
+  e->pool.push_back(fork);
+  k_finalize<<<1, 64, 0, s>>>(F);
+  NFSP_LAUNCHED("k_finalize");
+  return NFSP_OK;
+}
