@@ -303,46 +303,102 @@ struct ChainArgs {
   float lr_fixed;                 // AR lr
   double lr0;                     // BR: lr_u = lr0 / (1 + 0.003 sqrt(it0 + 2u))
   int64_t it0[2];
+  unsigned long long* stamps;     // diagnostic build only (NFSP_CHAIN_STAMPS): phase cycles
 };
+
+// In-kernel phase stamps (cdna_hip_programming.md §7): a separate diagnostic build only.
+#ifdef NFSP_CHAIN_STAMPS
+#define CHAIN_STAMP(k)                                                                   \
+  do {                                                                                  \
+    __builtin_amdgcn_sched_barrier(0);                                                  \
+    unsigned long long _t;                                                              \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");          \
+    __builtin_amdgcn_sched_barrier(0);                                                  \
+    st_acc[k] += _t - st_last;                                                          \
+    st_last = _t;                                                                       \
+  } while (0)
+#else
+#define CHAIN_STAMP(k) do { } while (0)
+#endif
+
+constexpr int ZROW = nfsp::OBS;            // an all-zero W1 row for padded gathers
+constexpr int W1ROWS = nfsp::OBS + 1;
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 struct ChainSmem {
-  float W1[nfsp::OBS * nn::H];
-  float gW1[4][nfsp::OBS * nn::H];
+  float W1[W1ROWS * nn::H];
+  float gW1[4][nfsp::OBS * nn::H];     // per-wave partial W1 gradients (fully rewritten)
   float gW2[4][nn::H * 3];
   float gb1[4][nn::H];
-  float gb2[4][3];
+  float gb2[4][4];
 };
 
-// sum over the 64 lanes of 24 values; afterwards lane l holds the sums of values
-// 3(l >> 3) + {0, 1, 2} (one 8-lane group per sample)
+// Wave-uniform W1 row offsets of the set bits of x (ascending), padded with the zero
+// row.  A Leduc observation has at most 9 set bits (<= 6 history + 3 card bits).
+__device__ inline void bit_rows(uint32_t x, int (&off)[9]) {
+#pragma unroll
+  for (int u = 0; u < 9; ++u) {
+    int i = ZROW;
+    if (x) {
+      i = __builtin_ctz(x);
+      x &= x - 1;
+    }
+    off[u] = i * nn::H;
+  }
+}
+
+__device__ inline float dpp_f(float x, int ctrl) {
+  switch (ctrl) {   // the control word must be an immediate
+    case 0x128: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x128, 0xF, 0xF, false));
+    case 0xB1: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xF, 0xF, false));
+    case 0x4E: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xF, 0xF, false));
+    default: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x141, 0xF, 0xF, false));
+  }
+}
+
+// Sum over the 64 lanes of 24 values, halving the live values at every exchange so the
+// whole reduction is 42 cross-lane VALU ops and no LDS traffic:
+//   v_permlane32_swap (lanes 32-63 <-> 0-31):  24 values -> 12 per lane
+//   v_permlane16_swap (odd <-> even 16-rows):  12 -> 6
+//   DPP row_ror:8 (= lane ^ 8 within a row):    6 -> 3
+//   DPP quad xor 1, quad xor 2, row_half_mirror: full sums inside each 8-lane group.
+// Afterwards lane l holds the sums of values 3(l >> 3) + {0, 1, 2}.
 __device__ inline void reduce24(float (&v)[24], float& s0, float& s1, float& s2) {
   const int lane = threadIdx.x & 63;
   float w12[12], w6[6], w3[3];
-  const bool h5 = lane & 32, h4 = lane & 16, h3 = lane & 8;
 #pragma unroll
   for (int i = 0; i < 12; ++i) {
-    const float keep = h5 ? v[i + 12] : v[i];
-    const float send = h5 ? v[i] : v[i + 12];
-    w12[i] = keep + __shfl_xor(send, 32, 64);
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 12]),
+                                                    false, false);
+    w12[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
   }
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
-    const float keep = h4 ? w12[i + 6] : w12[i];
-    const float send = h4 ? w12[i] : w12[i + 6];
-    w6[i] = keep + __shfl_xor(send, 16, 64);
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(w12[i]), __float_as_uint(w12[i + 6]),
+                                                    false, false);
+    w6[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
   }
+  const bool h3 = lane & 8;
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     const float keep = h3 ? w6[i + 3] : w6[i];
     const float send = h3 ? w6[i] : w6[i + 3];
-    w3[i] = keep + __shfl_xor(send, 8, 64);
+    w3[i] = keep + dpp_f(send, 0x128);
   }
 #pragma unroll
-  for (int d = 4; d >= 1; d >>= 1) {
-#pragma unroll
-    for (int i = 0; i < 3; ++i) w3[i] += __shfl_xor(w3[i], d, 64);
+  for (int i = 0; i < 3; ++i) {
+    w3[i] = w3[i] + dpp_f(w3[i], 0xB1);
+    w3[i] = w3[i] + dpp_f(w3[i], 0x4E);
+    w3[i] = w3[i] + dpp_f(w3[i], 0x141);
   }
   s0 = w3[0]; s1 = w3[1]; s2 = w3[2];
+}
+
+__device__ inline int64_t next_active(const ChainArgs& C, int64_t slot0, int64_t u, int64_t u1) {
+  if (C.active)
+    while (u < u1 && !C.active[slot0 + u]) ++u;
+  return u;
 }
 
 __global__ void __launch_bounds__(256) k_chain(ChainArgs C) {
@@ -352,11 +408,9 @@ __global__ void __launch_bounds__(256) k_chain(ChainArgs C) {
   const int tid = threadIdx.x;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int j = tid & 63;
+  const int myr = j >> 3;            // the sample whose loss this lane's 8-lane group computes
   float* gw = C.w[blockIdx.x];
-  for (int i = tid; i < nfsp::OBS * nn::H; i += 256) {
-    sm.W1[i] = gw[i];
-    sm.gW1[0][i] = 0.f; sm.gW1[1][i] = 0.f; sm.gW1[2][i] = 0.f; sm.gW1[3][i] = 0.f;
-  }
+  for (int i = tid; i < W1ROWS * nn::H; i += 256) sm.W1[i] = i < nfsp::OBS * nn::H ? gw[i] : 0.f;
   float b1 = gw[nn::OB1 + j];
   float W2_0 = gw[nn::OW2 + 3 * j + 0], W2_1 = gw[nn::OW2 + 3 * j + 1], W2_2 = gw[nn::OW2 + 3 * j + 2];
   float b2_0 = gw[nn::OB2 + 0], b2_1 = gw[nn::OB2 + 1], b2_2 = gw[nn::OB2 + 2];
@@ -364,143 +418,216 @@ __global__ void __launch_bounds__(256) k_chain(ChainArgs C) {
   const int nmb = C.B / CHAIN_MB;
   const float inv3m = 1.0f / (float)(3 * CHAIN_MB);
   const float invm = 1.0f / (float)CHAIN_MB;
-  for (int64_t u = C.u0[blockIdx.x]; u < C.u1[blockIdx.x]; ++u) {
-    const int64_t slot = (int64_t)a * C.umax + u;
-    if (C.active && !C.active[slot]) continue;
-    const float lr = C.relu ? (float)(C.lr0 / (1.0 + 0.003 * sqrt((double)(C.it0[blockIdx.x] + 2 * u))))
-                            : C.lr_fixed;
-    for (int e = 0; e < C.E; ++e) {
-      for (int s = 0; s < nmb; ++s) {
-        const FitRow* rows = C.fit + (slot * C.E + e) * C.B + s * CHAIN_MB + w * 8;
-        uint32_t xb[8];
-        float t[8][3];
+  const int64_t slot0 = (int64_t)a * C.umax;
+  const int64_t u1 = C.u1[blockIdx.x];
+  int64_t u = next_active(C, slot0, C.u0[blockIdx.x], u1);
+  int e = 0, s = 0;
+  // each lane prefetches (one step ahead) the row of ITS group's sample
+  uint4 pf = make_uint4(0, 0, 0, 0);
+  auto issue = [&](int64_t uu, int ee, int ss) {
+    const uint4* rows = reinterpret_cast<const uint4*>(C.fit + ((slot0 + uu) * C.E + ee) * C.B +
+                                                       ss * CHAIN_MB + w * 8);
+    pf = rows[myr];
+  };
+  if (u < u1) issue(u, e, s);
+  float lr = 0.f;
+#ifdef NFSP_CHAIN_STAMPS
+  unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_last = 0;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
+#endif
+  while (u < u1) {
+    const uint32_t xs = pf.x;                       // my group's sample
+    const float tt0 = __uint_as_float(pf.y), tt1 = __uint_as_float(pf.z), tt2 = __uint_as_float(pf.w);
+    uint32_t xb[8];
 #pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          xb[r] = __builtin_amdgcn_readfirstlane(rows[r].x);
-          t[r][0] = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(rows[r].t0)));
-          t[r][1] = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(rows[r].t1)));
-          t[r][2] = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(rows[r].t2)));
-        }
-        // ---- forward
-        float z1[8];
-        float v[24];
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          float acc = 0.f;
-          uint32_t bits = xb[r];
-          while (bits) {
-            const int i = __builtin_ctz(bits);
-            bits &= bits - 1;
-            acc = acc + sm.W1[i * nn::H + j];
-          }
-          z1[r] = acc + b1;
-          const float h = z1[r] > 0.f ? z1[r] : 0.f;
-          v[3 * r + 0] = h * W2_0;
-          v[3 * r + 1] = h * W2_1;
-          v[3 * r + 2] = h * W2_2;
-        }
-        float s0, s1, s2;
-        reduce24(v, s0, s1, s2);
-        // ---- loss gradient dL/dz2 (uniform per sample)
-        float d[8][3];
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          const float o0 = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(s0), 8 * r)) + b2_0;
-          const float o1 = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(s1), 8 * r)) + b2_1;
-          const float o2 = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(s2), 8 * r)) + b2_2;
-          const float zz[3] = {o0, o1, o2};
-          if (C.relu) {
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-              const float y = zz[k] > 0.f ? zz[k] : 0.f;
-              const float ee = t[r][k] - y;
-              const float g = fabsf(ee) > 1.0f ? (ee > 0.f ? 1.f : (ee < 0.f ? -1.f : 0.f)) : ee;
-              d[r][k] = zz[k] > 0.f ? (-g * inv3m) : 0.f;
-            }
-          } else {
-            const float mx = fmaxf(fmaxf(o0, o1), o2);
-            const float e0 = expf(o0 - mx), e1 = expf(o1 - mx), e2 = expf(o2 - mx);
-            const float ssum = (e0 + e1) + e2;
-            const float y[3] = {e0 / ssum, e1 / ssum, e2 / ssum};
-            const float S = (y[0] + y[1]) + y[2];
-            const float eps = 1e-7f, hi = 1.0f - 1e-7f;
-            float dp[3];
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-              const float p = y[k] / S;
-              const float pc = fminf(fmaxf(p, eps), hi);
-              const float msk = (p >= eps && p <= hi) ? 1.f : 0.f;
-              dp[k] = (-t[r][k] / pc) * msk * invm;
-            }
-            const float dpy = (dp[0] * y[0] + dp[1] * y[1]) + dp[2] * y[2];
-            float dy[3];
-#pragma unroll
-            for (int k = 0; k < 3; ++k) dy[k] = dp[k] / S - dpy / (S * S);
-            const float dyy = (dy[0] * y[0] + dy[1] * y[1]) + dy[2] * y[2];
-#pragma unroll
-            for (int k = 0; k < 3; ++k) d[r][k] = y[k] * (dy[k] - dyy);
-          }
-        }
-        // ---- backward
-        float g2_0 = 0.f, g2_1 = 0.f, g2_2 = 0.f, gb1 = 0.f, gb2_0 = 0.f, gb2_1 = 0.f, gb2_2 = 0.f;
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          const float h = z1[r] > 0.f ? z1[r] : 0.f;
-          g2_0 += h * d[r][0];
-          g2_1 += h * d[r][1];
-          g2_2 += h * d[r][2];
-          gb2_0 += d[r][0];
-          gb2_1 += d[r][1];
-          gb2_2 += d[r][2];
-          const float dh = (d[r][0] * W2_0 + d[r][1] * W2_1) + d[r][2] * W2_2;
-          const float dz = z1[r] > 0.f ? dh : 0.f;
-          gb1 += dz;
-          uint32_t bits = xb[r];
-          while (bits) {
-            const int i = __builtin_ctz(bits);
-            bits &= bits - 1;
-            sm.gW1[w][i * nn::H + j] += dz;      // this lane owns column j of wave w's partial
-          }
-        }
-        sm.gW2[w][3 * j + 0] = g2_0;
-        sm.gW2[w][3 * j + 1] = g2_1;
-        sm.gW2[w][3 * j + 2] = g2_2;
-        sm.gb1[w][j] = gb1;
-        if (j == 0) {
-          sm.gb2[w][0] = gb2_0;
-          sm.gb2[w][1] = gb2_1;
-          sm.gb2[w][2] = gb2_2;
-        }
-        __syncthreads();
-        // ---- SGD update (fixed reduction order over the 4 wave partials)
-        for (int i = tid; i < nfsp::OBS * nn::H; i += 256) {
-          const float g = ((sm.gW1[0][i] + sm.gW1[1][i]) + sm.gW1[2][i]) + sm.gW1[3][i];
-          sm.W1[i] = sm.W1[i] - lr * g;
-          sm.gW1[0][i] = 0.f; sm.gW1[1][i] = 0.f; sm.gW1[2][i] = 0.f; sm.gW1[3][i] = 0.f;
-        }
-        {
-          float g0 = ((sm.gW2[0][3 * j] + sm.gW2[1][3 * j]) + sm.gW2[2][3 * j]) + sm.gW2[3][3 * j];
-          float g1 = ((sm.gW2[0][3 * j + 1] + sm.gW2[1][3 * j + 1]) + sm.gW2[2][3 * j + 1]) +
-                     sm.gW2[3][3 * j + 1];
-          float g2 = ((sm.gW2[0][3 * j + 2] + sm.gW2[1][3 * j + 2]) + sm.gW2[2][3 * j + 2]) +
-                     sm.gW2[3][3 * j + 2];
-          const float gb = ((sm.gb1[0][j] + sm.gb1[1][j]) + sm.gb1[2][j]) + sm.gb1[3][j];
-          W2_0 = W2_0 - lr * g0;
-          W2_1 = W2_1 - lr * g1;
-          W2_2 = W2_2 - lr * g2;
-          b1 = b1 - lr * gb;
-          g0 = ((sm.gb2[0][0] + sm.gb2[1][0]) + sm.gb2[2][0]) + sm.gb2[3][0];
-          g1 = ((sm.gb2[0][1] + sm.gb2[1][1]) + sm.gb2[2][1]) + sm.gb2[3][1];
-          g2 = ((sm.gb2[0][2] + sm.gb2[1][2]) + sm.gb2[2][2]) + sm.gb2[3][2];
-          b2_0 = b2_0 - lr * g0;
-          b2_1 = b2_1 - lr * g1;
-          b2_2 = b2_2 - lr * g2;
-        }
-        __syncthreads();
+    for (int r = 0; r < 8; ++r) xb[r] = __builtin_amdgcn_readlane(xs, 8 * r);
+    CHAIN_STAMP(0);
+    if (e == 0 && s == 0)
+      lr = C.relu ? (float)(C.lr0 / (1.0 + 0.003 * sqrt((double)(C.it0[blockIdx.x] + 2 * u)))) : C.lr_fixed;
+    // advance (u, e, s) and prefetch the next step's row
+    int64_t nu = u;
+    int ne = e, ns = s + 1;
+    if (ns == nmb) {
+      ns = 0;
+      if (++ne == C.E) {
+        ne = 0;
+        nu = next_active(C, slot0, u + 1, u1);
       }
     }
+    if (nu < u1) issue(nu, ne, ns);
+    CHAIN_STAMP(1);
+    // ---- forward: padded, branch-free gathers of the set bits' W1 rows
+    float z1[8];
+    float v[24];
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      int off[4][9];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bit_rows(xb[4 * hh + r], off[r]);
+      float wv[4][9];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int q = 0; q < 9; ++q) wv[r][q] = sm.W1[off[r][q] + j];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float acc = 0.f;
+#pragma unroll
+        for (int q = 0; q < 9; ++q) acc = acc + wv[r][q];
+        const int rr = 4 * hh + r;
+        z1[rr] = acc + b1;
+        const float h = z1[rr] > 0.f ? z1[rr] : 0.f;
+        v[3 * rr + 0] = h * W2_0;
+        v[3 * rr + 1] = h * W2_1;
+        v[3 * rr + 2] = h * W2_2;
+      }
+    }
+    CHAIN_STAMP(2);
+    float s0, s1, s2;
+    reduce24(v, s0, s1, s2);          // lane group g now holds sample g's three sums
+    CHAIN_STAMP(3);
+    // ---- loss gradient of my group's sample, then broadcast all 8 samples' to SGPRs
+    float d0, d1, d2;
+    {
+      const float o0 = s0 + b2_0, o1 = s1 + b2_1, o2 = s2 + b2_2;
+      if (C.relu) {
+        const float zz[3] = {o0, o1, o2}, tt[3] = {tt0, tt1, tt2};
+        float dd[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const float y = zz[k] > 0.f ? zz[k] : 0.f;
+          const float ee = tt[k] - y;
+          const float g = fabsf(ee) > 1.0f ? (ee > 0.f ? 1.f : (ee < 0.f ? -1.f : 0.f)) : ee;
+          dd[k] = zz[k] > 0.f ? (-g * inv3m) : 0.f;
+        }
+        d0 = dd[0]; d1 = dd[1]; d2 = dd[2];
+      } else {
+        const float mx = fmaxf(fmaxf(o0, o1), o2);
+        const float e0 = expf(o0 - mx), e1 = expf(o1 - mx), e2 = expf(o2 - mx);
+        const float ssum = (e0 + e1) + e2;
+        const float y[3] = {e0 / ssum, e1 / ssum, e2 / ssum};
+        const float S = (y[0] + y[1]) + y[2];
+        const float eps = 1e-7f, hi = 1.0f - 1e-7f;
+        const float tt[3] = {tt0, tt1, tt2};
+        float dp[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const float p = y[k] / S;
+          const float pc = fminf(fmaxf(p, eps), hi);
+          const float msk = (p >= eps && p <= hi) ? 1.f : 0.f;
+          dp[k] = (-tt[k] / pc) * msk * invm;
+        }
+        const float dpy = (dp[0] * y[0] + dp[1] * y[1]) + dp[2] * y[2];
+        float dy[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) dy[k] = dp[k] / S - dpy / (S * S);
+        const float dyy = (dy[0] * y[0] + dy[1] * y[1]) + dy[2] * y[2];
+        d0 = y[0] * (dy[0] - dyy);
+        d1 = y[1] * (dy[1] - dyy);
+        d2 = y[2] * (dy[2] - dyy);
+      }
+    }
+    float dr[8][3];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      dr[r][0] = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(d0), 8 * r));
+      dr[r][1] = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(d1), 8 * r));
+      dr[r][2] = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(d2), 8 * r));
+    }
+    CHAIN_STAMP(4);
+    // ---- backward: layer 2 / biases on the VALU, W1 gradient (X^T dZ1) on MFMA
+    float g2_0 = 0.f, g2_1 = 0.f, g2_2 = 0.f, gb1 = 0.f, gb2_0 = 0.f, gb2_1 = 0.f, gb2_2 = 0.f;
+    float dz1[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const float h = z1[r] > 0.f ? z1[r] : 0.f;
+      g2_0 += h * dr[r][0];
+      g2_1 += h * dr[r][1];
+      g2_2 += h * dr[r][2];
+      gb2_0 += dr[r][0];
+      gb2_1 += dr[r][1];
+      gb2_2 += dr[r][2];
+      const float dh = (dr[r][0] * W2_0 + dr[r][1] * W2_1) + dr[r][2] * W2_2;
+      dz1[r] = z1[r] > 0.f ? dh : 0.f;
+      gb1 += dz1[r];
+    }
+    // v_mfma_f32_32x32x2_f32, k = sample pair (2c, 2c+1): A[i][k] = bit i of x_{2c+k}
+    // (lane: i = l & 31, k = l >> 5); B[k][n] = dZ1[2c+k][32 t + n] for tile t, built
+    // from the lane-major dz1 registers by one permlane32 swap.
+    floatx16 acc0 = {}, acc1 = {};
+    const bool hiw = j >= 32;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const uint32_t xsel = hiw ? xb[2 * c + 1] : xb[2 * c];
+      const float av = ((xsel >> (j & 31)) & 1u) ? 1.f : 0.f;
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(dz1[2 * c]),
+                                                       __float_as_uint(dz1[2 * c + 1]), false, false);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av, __uint_as_float(sw[0]), acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av, __uint_as_float(sw[1]), acc1, 0, 0, 0);
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int row = (k & 3) + 8 * (k >> 2) + 4 * (j >> 5);
+      if (row < nfsp::OBS) {
+        sm.gW1[w][row * nn::H + (j & 31)] = acc0[k];
+        sm.gW1[w][row * nn::H + 32 + (j & 31)] = acc1[k];
+      }
+    }
+    sm.gW2[w][3 * j + 0] = g2_0;
+    sm.gW2[w][3 * j + 1] = g2_1;
+    sm.gW2[w][3 * j + 2] = g2_2;
+    sm.gb1[w][j] = gb1;
+    if (j == 0) {
+      sm.gb2[w][0] = gb2_0;
+      sm.gb2[w][1] = gb2_1;
+      sm.gb2[w][2] = gb2_2;
+    }
+    CHAIN_STAMP(5);
+    __syncthreads();
+    CHAIN_STAMP(6);
+    // ---- SGD update (fixed reduction order over the 4 wave partials)
+    {
+      float g[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int i = tid + 256 * k;
+        g[k] = 0.f;
+        if (i < nfsp::OBS * nn::H) g[k] = ((sm.gW1[0][i] + sm.gW1[1][i]) + sm.gW1[2][i]) + sm.gW1[3][i];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int i = tid + 256 * k;
+        if (i < nfsp::OBS * nn::H) sm.W1[i] = sm.W1[i] - lr * g[k];
+      }
+      float g0 = ((sm.gW2[0][3 * j] + sm.gW2[1][3 * j]) + sm.gW2[2][3 * j]) + sm.gW2[3][3 * j];
+      float g1 = ((sm.gW2[0][3 * j + 1] + sm.gW2[1][3 * j + 1]) + sm.gW2[2][3 * j + 1]) +
+                 sm.gW2[3][3 * j + 1];
+      float g2 = ((sm.gW2[0][3 * j + 2] + sm.gW2[1][3 * j + 2]) + sm.gW2[2][3 * j + 2]) +
+                 sm.gW2[3][3 * j + 2];
+      const float gb = ((sm.gb1[0][j] + sm.gb1[1][j]) + sm.gb1[2][j]) + sm.gb1[3][j];
+      W2_0 = W2_0 - lr * g0;
+      W2_1 = W2_1 - lr * g1;
+      W2_2 = W2_2 - lr * g2;
+      b1 = b1 - lr * gb;
+      g0 = ((sm.gb2[0][0] + sm.gb2[1][0]) + sm.gb2[2][0]) + sm.gb2[3][0];
+      g1 = ((sm.gb2[0][1] + sm.gb2[1][1]) + sm.gb2[2][1]) + sm.gb2[3][1];
+      g2 = ((sm.gb2[0][2] + sm.gb2[1][2]) + sm.gb2[2][2]) + sm.gb2[3][2];
+      b2_0 = b2_0 - lr * g0;
+      b2_1 = b2_1 - lr * g1;
+      b2_2 = b2_2 - lr * g2;
+    }
+    CHAIN_STAMP(7);
+    __syncthreads();
+    CHAIN_STAMP(8);
+    u = nu;
+    e = ne;
+    s = ns;
   }
-  // write back (wave 0 holds the replicated small parameters)
+#ifdef NFSP_CHAIN_STAMPS
+  if (C.stamps && j == 0)
+    for (int k = 0; k < 10; ++k) C.stamps[(blockIdx.x * 4 + w) * 10 + k] = st_acc[k];
+#endif
+  // write back (every wave holds identical copies of the small parameters)
   float* dsts[2] = {gw, C.sync_to[blockIdx.x]};
   for (int k = 0; k < 2; ++k) {
     float* dst = dsts[k];

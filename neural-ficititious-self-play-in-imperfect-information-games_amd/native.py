@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libnfsp.so")
+LIB_PATH = os.environ.get("NFSP_LIB", os.path.join(HERE, "libnfsp.so"))
 
 OK, EINVAL, EHIP, ENOMEM = 0, -1, -2, -3
 GAME_LEDUC = 0
