@@ -46,25 +46,37 @@ int main(int argc, char** argv) {
   C.w[0] = dw; C.sync_to[0] = nullptr; C.fit = dfit; C.active = nullptr; C.umax = U;
   C.u0[0] = 0; C.u1[0] = U; C.agents[0] = 0; C.B = B; C.E = E; C.relu = relu;
   C.lr_fixed = 0.1f; C.lr0 = 0.05; C.it0[0] = 0; C.stamps = dst;
+  const int variant = argc > 3 ? atoi(argv[3]) : 2;
   CK(hipFuncSetAttribute((const void*)k_chain, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(ChainSmem)));
+  auto launch = [&]() {
+    if (variant == 2) k_chain2<<<1, 256, sizeof(Chain2Smem)>>>(C);
+    else k_chain<<<1, 256, sizeof(ChainSmem)>>>(C);
+  };
   hipEvent_t a, b;
   CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
-  k_chain<<<1, 256, sizeof(ChainSmem)>>>(C);   // warm
+  launch();   // warm
   CK(hipDeviceSynchronize());
   CK(hipMemcpy(dw, w.data(), w.size() * 4, hipMemcpyHostToDevice));
   CK(hipMemset(dst, 0, 80 * 8));
   CK(hipEventRecord(a));
-  k_chain<<<1, 256, sizeof(ChainSmem)>>>(C);
+  launch();
   CK(hipEventRecord(b));
   CK(hipEventSynchronize(b));
   float ms; CK(hipEventElapsedTime(&ms, a, b));
   const int steps = U * E * (B / 32);
+  std::vector<float> wout(nn::NP);
+  CK(hipMemcpy(wout.data(), dw, wout.size() * 4, hipMemcpyDeviceToHost));
+  double cs = 0; for (float v : wout) cs += v;
+  printf("variant=%d checksum=%.9g ", variant, cs);
   printf("relu=%d updates=%d sgd_steps=%d  %.3f ms  %.3f us/step  %.2f us/update\n", relu, U, steps, ms,
          ms * 1e3 / steps, ms * 1e3 / U);
   std::vector<unsigned long long> st(80);
   CK(hipMemcpy(st.data(), dst, 80 * 8, hipMemcpyDeviceToHost));
-  const char* names[10] = {"rows", "lr+prefetch", "fwd", "reduce24", "loss", "backward", "barrier1",
-                           "update", "barrier2", "-"};
+  const char* names1[10] = {"rows", "lr+prefetch", "fwd", "reduce24", "loss", "backward", "barrier1",
+                            "update", "barrier2", "-"};
+  const char* names2[10] = {"rows+masks", "fwd-mfma", "layer2+po", "barrier", "loss+gb2", "bwd-valu",
+                            "mfma-dW1+upd", "-", "-", "-"};
+  const char** names = variant == 2 ? names2 : names1;
   for (int wv = 0; wv < 4; ++wv) {
     unsigned long long tot = 0;
     for (int k = 0; k < 9; ++k) tot += st[wv * 10 + k];
