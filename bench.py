@@ -51,9 +51,21 @@ BYTES_RL, BYTES_SL = 257, 132            # reference tuple layout in fp32 (SURVE
 
 
 def learner_flops(br_updates, ar_updates, batch=128, epochs=2):
-    br = br_updates * (2 * batch * F_FWD + epochs * batch * F_TRAIN)
+    br = br_updates * (2 * batch * F_FWD + epochs * batch * F_TRAIN)   # targets + fit
     ar = ar_updates * (epochs * batch * F_TRAIN)
     return br + ar
+
+
+def load_pmc(config, kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC summary of this config
+    (FETCH_SIZE x 2 + WRITE_SIZE, KB -> bytes; MI355X_MICROARCH.md §HBM), or None."""
+    path = os.path.join(REPO, "profiles", f"pmc_{config}.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    k = d.get("kernels", {}).get(kernel)
+    return None if k is None else k.get("hbm_bytes_per_launch")
 
 
 def cpu_baseline(seconds: float):
@@ -138,9 +150,7 @@ def main():
     rl_ins = sum(s1["rl_total"]) - sum(s0["rl_total"])
     sl_ins = sum(s1["sl_total"]) - sum(s0["sl_total"])
     k_ms = {k: v[0] / max(v[1], 1) for k, v in timings.items()}
-    # dominant kernel by total time in the timed region
-    dom = max(timings, key=lambda k: timings[k][0])
-    flops_learner = learner_flops(br_upd, ar_upd) / max(timings["k_learner"][1], 1)
+    k_launches = {k: v[1] for k, v in timings.items()}
     t_rl, t_sl = rl_ins / hands_rank, sl_ins / hands_rank
     bytes_hand = BYTES_RL * t_rl + BYTES_SL * t_sl
     rollout_bytes = bytes_hand * cfg["n_lanes"]
@@ -149,14 +159,25 @@ def main():
                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "traffic": None,
                     "bytes_per_hand": bytes_hand, "avg_ms": k_ms["k_rollout"]}
     roof_rollout["frac"] = roof_rollout["achieved"] / PEAK_HBM_GBS
-    if dom == "k_learner":
-        ach = flops_learner / (k_ms["k_learner"] * 1e-3) / 1e12
-        roofline = {"kernel": "k_learner", "bound": "mfma", "achieved": ach,
-                    "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s", "frac": ach / PEAK_FP32_TFLOPS,
-                    "traffic": None, "avg_ms": k_ms["k_learner"],
-                    "flop_per_launch": flops_learner}
-    else:
-        roofline = dict(roof_rollout)
+
+    def chain_roof(name, updates):
+        n = max(k_launches[name], 1)
+        flop = updates * 2 * 128 * F_TRAIN / n            # epochs x batch rows x F_TRAIN
+        ach = flop / (k_ms[name] * 1e-3) / 1e12 if k_ms[name] > 0 else 0.0
+        return {"kernel": name, "bound": "mfma", "achieved": ach, "peak": PEAK_FP32_TFLOPS,
+                "unit": "TFLOP/s", "frac": ach / PEAK_FP32_TFLOPS, "traffic": None,
+                "avg_ms": k_ms[name], "launches": k_launches[name], "flop_per_launch": flop}
+    roofs = {"k_chain2_br": chain_roof("k_chain2_br", br_upd),
+             "k_chain2_ar": chain_roof("k_chain2_ar", ar_upd),
+             "k_rollout": roof_rollout}
+    # the dominant kernel = largest GPU time inside the timed region
+    singles = [k for k in timings if k != "learner"]
+    dom = max(singles, key=lambda k: timings[k][0])
+    roofline = dict(roofs.get(dom, roof_rollout))
+    pmc = load_pmc(args.config, roofline["kernel"])
+    if pmc is not None:
+        roofline["traffic"] = pmc
+        roofline["traffic_source"] = f"profiles/pmc_{args.config}.json (rocprofv3 --pmc passes)"
     rollout_path_ms = k_ms["k_rollout"] + k_ms["k_scan"] + k_ms["k_commit"]
     out = {
         "metric": "Leduc self-play hands/sec",
@@ -175,7 +196,7 @@ def main():
                    "rl_capacity": cfg["rl_capacity"], "sl_capacity": cfg["sl_capacity"],
                    "inserts_per_update": 128, "batch": 128, "parallelism": f"replicas x{world}"},
         "roofline": roofline,
-        "roofline_rollout": roof_rollout,
+        "roofline_other": {k: v for k, v in roofs.items() if k != roofline["kernel"]},
         "kernel_ms": k_ms,
         "rollout_only_hands_per_s": cfg["n_lanes"] / (rollout_path_ms * 1e-3) * world,
         "per_step": {"br_updates": br_upd / args.steps, "ar_updates": ar_upd / args.steps,

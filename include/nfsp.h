@@ -210,11 +210,13 @@ int nfsp_engine_get_stats(nfsp_engine* e, nfsp_engine_stats* out);   /* synchron
 int nfsp_engine_memories(nfsp_engine* e, int agent, nfsp_records* rl, int64_t* rl_log_cap,
                          nfsp_records* sl, uint32_t** dev_pending_sl_obs,
                          float** dev_pending_sl_a, int64_t** dev_pending_sl_rl_pos);
-/* Per-kernel timing with HIP events recorded on the ctx stream around each launch:
- * ms / launches [4] = {k_rollout, k_scan1+k_scan2, k_commit, k_learner}, accumulated since
- * the previous nfsp_engine_get_timings (which synchronises and resets them). */
+/* Per-kernel timing with HIP events recorded around each launch on the stream it runs on:
+ * ms / launches [8] = {k_rollout, k_scan1+k_scan2, k_commit, learner (whole
+ * nfsp_engine_update), learner prep (k_br_prep..k_res_apply), k_br_targets,
+ * k_chain2<BR>, k_chain2<AR>}, accumulated since the previous nfsp_engine_get_timings
+ * (which synchronises and resets them). */
 int nfsp_engine_set_timing(nfsp_engine* e, int on);
-int nfsp_engine_get_timings(nfsp_engine* e, double* ms /*[4]*/, int64_t* launches /*[4]*/);
+int nfsp_engine_get_timings(nfsp_engine* e, double* ms /*[8]*/, int64_t* launches /*[8]*/);
 /* Debug view of the last learner run: per agent and role (0 = AR, 1 = BR) the sampled
  * rows [batch] (int64) and fit permutations [epochs][batch] (int32) of its LAST update. */
 int nfsp_engine_last_update(nfsp_engine* e, int agent, int role, int64_t** dev_rows,

@@ -94,7 +94,11 @@ struct LearnBufs {
   int32_t* res_slot;   // [2][pend_cap]
 };
 
-enum { KT_ROLLOUT = 0, KT_SCAN = 1, KT_COMMIT = 2, KT_LEARNER = 3, KT_N = 4 };
+// per-kernel timing slots (nfsp_engine_get_timings)
+enum {
+  KT_ROLLOUT = 0, KT_SCAN = 1, KT_COMMIT = 2, KT_LEARNER = 3,   // LEARNER = whole update call
+  KT_PREP = 4, KT_TARGETS = 5, KT_CHAIN_BR = 6, KT_CHAIN_AR = 7, KT_N = 8
+};
 
 // Stage packed weights (W1[30][64] | b1 | W2 | b2) into the padded LDS layout of fwd_lds.
 __device__ inline void stage_net_lds(float* sw, const float* __restrict__ w, int tid, int nt) {
@@ -185,21 +189,22 @@ namespace eng {
 
 hipEvent_t take_event(nfsp_engine* e);
 
-// RAII bracket: records start/stop events around launches when timing is on
+// RAII bracket: records start/stop events around launches on `stream` when timing is on
 struct KTimer {
   nfsp_engine* e;
   int id;
+  hipStream_t st;
   hipEvent_t a = nullptr;
-  KTimer(nfsp_engine* e_, int id_) : e(e_), id(id_) {
+  KTimer(nfsp_engine* e_, int id_, hipStream_t s_ = nullptr) : e(e_), id(id_), st(s_ ? s_ : e_->ctx->stream) {
     if (e->timing) {
       a = take_event(e);
-      (void)hipEventRecord(a, e->ctx->stream);
+      (void)hipEventRecord(a, st);
     }
   }
   ~KTimer() {
     if (e->timing) {
       hipEvent_t b = take_event(e);
-      (void)hipEventRecord(b, e->ctx->stream);
+      (void)hipEventRecord(b, st);
       e->marks.push_back({id, {a, b}});
     }
   }

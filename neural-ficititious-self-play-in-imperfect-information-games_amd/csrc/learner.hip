@@ -686,6 +686,7 @@ __device__ inline float sum_x16(float x) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
+template <int RELU>
 __global__ void __launch_bounds__(256) k_chain2(ChainArgs C) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   Chain2Smem& sm = *reinterpret_cast<Chain2Smem*>(smem_raw);
@@ -729,7 +730,7 @@ __global__ void __launch_bounds__(256) k_chain2(ChainArgs C) {
     const float tt0 = __uint_as_float(pf.y), tt1 = __uint_as_float(pf.z), tt2 = __uint_as_float(pf.w);
     if (l < 32) sm.xm[w][l] = myx;
     if (e == 0 && s == 0)
-      lr = C.relu ? (float)(C.lr0 / (1.0 + 0.003 * sqrt((double)(C.it0[blockIdx.x] + 2 * u)))) : C.lr_fixed;
+      lr = RELU ? (float)(C.lr0 / (1.0 + 0.003 * sqrt((double)(C.it0[blockIdx.x] + 2 * u)))) : C.lr_fixed;
     int64_t nu = u;
     int ne = e, ns = s + 1;
     if (ns == nmb) {
@@ -803,7 +804,7 @@ __global__ void __launch_bounds__(256) k_chain2(ChainArgs C) {
       const float o0 = (((p0.x + p1.x) + p2.x) + p3.x) + b2_0;
       const float o1 = (((p0.y + p1.y) + p2.y) + p3.y) + b2_1;
       const float o2 = (((p0.z + p1.z) + p2.z) + p3.z) + b2_2;
-      if (C.relu) {
+      if (RELU) {
         const float oz[3] = {o0, o1, o2}, tt[3] = {tt0, tt1, tt2};
         float dd[3];
 #pragma unroll
@@ -1002,6 +1003,8 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
     maxSL = pl.n_sl > maxSL ? pl.n_sl : maxSL;
   }
   // ---- parallel prep on the ctx stream
+  {
+  KTimer kprep(e, KT_PREP);
   if (maxUbr > 0) {
     k_br_prep<<<dim3((unsigned)maxUbr, 2), 128, 0, s>>>(P);
     NFSP_LAUNCHED("k_br_prep");
@@ -1018,9 +1021,12 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
     k_res_apply<<<dim3(nfsp_blocks(maxSL, 256), 2), 256, 0, s>>>(P);
     NFSP_LAUNCHED("k_res_apply");
   }
+  }
   static bool attr = false;
   if (!attr) {
-    NFSP_HIP(hipFuncSetAttribute((const void*)k_chain2, hipFuncAttributeMaxDynamicSharedMemorySize,
+    NFSP_HIP(hipFuncSetAttribute((const void*)k_chain2<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 (int)sizeof(Chain2Smem)));
+    NFSP_HIP(hipFuncSetAttribute((const void*)k_chain2<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                  (int)sizeof(Chain2Smem)));
     attr = true;
   }
@@ -1044,7 +1050,8 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
       C.u0[a] = 0;
       C.u1[a] = P.A[a].U;
     }
-    k_chain2<<<2, 256, sizeof(Chain2Smem), e->s_ar>>>(C);
+    KTimer kc(e, KT_CHAIN_AR, e->s_ar);
+    k_chain2<0><<<2, 256, sizeof(Chain2Smem), e->s_ar>>>(C);
     NFSP_LAUNCHED("k_chain(AR)");
   }
   // ---- BR: per agent, segments between target syncs, each = targets + chain
@@ -1075,8 +1082,11 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
         ++v;
         if (s_here) { sync = true; break; }
       }
-      k_br_targets<<<(unsigned)(v - u), 128, 0, sa>>>(e->LB, wtg, a, u, cfg.batch, cfg.epochs,
-                                                       cfg.gamma, cfg.quirks);
+      {
+        KTimer kt2(e, KT_TARGETS, sa);
+        k_br_targets<<<(unsigned)(v - u), 128, 0, sa>>>(e->LB, wtg, a, u, cfg.batch, cfg.epochs,
+                                                         cfg.gamma, cfg.quirks);
+      }
       NFSP_LAUNCHED("k_br_targets");
       ChainArgs C{};
       C.fit = e->LB.br_fit;
@@ -1092,7 +1102,10 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
       C.u0[0] = u;
       C.u1[0] = v;
       C.it0[0] = it0;
-      k_chain2<<<1, 256, sizeof(Chain2Smem), sa>>>(C);
+      {
+        KTimer kc(e, KT_CHAIN_BR, sa);
+        k_chain2<1><<<1, 256, sizeof(Chain2Smem), sa>>>(C);
+      }
       NFSP_LAUNCHED("k_chain(BR)");
       u = v;
     }

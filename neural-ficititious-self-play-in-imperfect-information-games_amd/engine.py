@@ -96,15 +96,16 @@ class SelfPlayEngine:
         native.check(self.L.nfsp_engine_get_stats(self.h, C.byref(s)), "nfsp_engine_get_stats")
         return s.to_dict()
 
-    KERNELS = ("k_rollout", "k_scan", "k_commit", "k_learner")
+    KERNELS = ("k_rollout", "k_scan", "k_commit", "learner", "learner_prep", "k_br_targets",
+               "k_chain2_br", "k_chain2_ar")
 
     def set_timing(self, on=True):
         native.check(self.L.nfsp_engine_set_timing(self.h, int(bool(on))), "set_timing")
 
     def timings(self) -> dict:
         """{kernel: (total ms, launches)} since the last call (HIP events, ctx stream)."""
-        ms = (native.F64 * 4)()
-        n = (native.I64 * 4)()
+        ms = (native.F64 * 8)()
+        n = (native.I64 * 8)()
         native.check(self.L.nfsp_engine_get_timings(self.h, ms, n), "get_timings")
         return {k: (ms[i], n[i]) for i, k in enumerate(self.KERNELS)}
 

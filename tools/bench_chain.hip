@@ -49,7 +49,8 @@ int main(int argc, char** argv) {
   const int variant = argc > 3 ? atoi(argv[3]) : 2;
   CK(hipFuncSetAttribute((const void*)k_chain, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(ChainSmem)));
   auto launch = [&]() {
-    if (variant == 2) k_chain2<<<1, 256, sizeof(Chain2Smem)>>>(C);
+    if (variant == 2 && relu) k_chain2<1><<<1, 256, sizeof(Chain2Smem)>>>(C);
+    else if (variant == 2) k_chain2<0><<<1, 256, sizeof(Chain2Smem)>>>(C);
     else k_chain<<<1, 256, sizeof(ChainSmem)>>>(C);
   };
   hipEvent_t a, b;
