@@ -88,6 +88,9 @@ struct LearnBufs {
   double* br_expl;     // [2][umax]
   FitRow* br_fit;      // [2][umax][epochs][batch]
   FitRow* ar_fit;      // [2][umax][epochs][batch]
+  uint32_t* br_xt;     // [2][umax][epochs][batch / 32][32]: per minibatch, the mask over its
+  uint32_t* ar_xt;     //   32 samples of every input (bit-transposed x), the dW1 operand
+  float* br_lr;        // [2][umax] per-update BR learning rate (agent/agent.py:249)
   uint8_t* ar_active;  // [2][umax]
   unsigned long long* res_head;   // [2][sl_cap]  (tag << 32 | q)
   int32_t* res_next;   // [2][pend_cap]

@@ -124,6 +124,25 @@ __global__ void __launch_bounds__(256) k_ar_slots(PrepArgs P) {
   }
 }
 
+// Bit-transposed minibatch masks for the chain's dW1 operand: thread b holds the mask of
+// fit position b of one (update, epoch) block (0 for b >= B); writes xt[mb][i] = bit i of
+// the masks of minibatch mb's 32 rows (bit k = row 32 mb + k).  Whole block (a multiple of
+// 64 threads) calls.
+__device__ inline void emit_xt(uint32_t* __restrict__ xt, uint32_t x, int B) {
+  const int lane = threadIdx.x & 63;
+  unsigned long long mine = 0;
+#pragma unroll
+  for (int i = 0; i < nfsp::OBS; ++i) {
+    const unsigned long long m = __ballot((x >> i) & 1u);
+    if (lane == i) mine = m;
+  }
+  const int mb = (threadIdx.x >> 6) * 2;
+  if (lane < 32) {
+    if (32 * mb < B) xt[mb * 32 + lane] = (uint32_t)mine;
+    if (32 * (mb + 1) < B) xt[(mb + 1) * 32 + lane] = (uint32_t)(mine >> 32);
+  }
+}
+
 // latest insert of this rollout into `slot` with index < limit (-1: none)
 __device__ inline int64_t latest_insert(const LearnBufs& LB, const Memories& M, int a, int64_t slot,
                                         int64_t limit, uint32_t tag) {
@@ -146,6 +165,7 @@ __global__ void __launch_bounds__(128) k_ar_prep(PrepArgs P) {
   __shared__ uint32_t key[MAX_BATCH];
   __shared__ uint32_t rx[MAX_BATCH];
   __shared__ float ra[MAX_BATCH][3];
+  __shared__ uint32_t px[MAX_BATCH];
   __shared__ int64_t s_nb;
   const int a = blockIdx.y;
   const int64_t u = blockIdx.x;
@@ -204,8 +224,12 @@ __global__ void __launch_bounds__(128) k_ar_prep(PrepArgs P) {
       fr.x = rx[b];
       fr.t0 = ra[b][0]; fr.t1 = ra[b][1]; fr.t2 = ra[b][2];
       P.LB.ar_fit[(slot_u * P.E + e) * P.B + rank] = fr;
+      px[rank] = fr.x;
       if (last) P.M.dbg_perms[(dbg * P.E + e) * P.B + rank] = b;
     }
+    __syncthreads();
+    emit_xt(P.LB.ar_xt + (slot_u * P.E + e) * P.B, b < P.B ? px[b] : 0u, P.B);
+    __syncthreads();
   }
   if (last && b < P.B) P.M.dbg_rows[dbg * P.B + b] = cand[b];
 }
@@ -231,7 +255,7 @@ __global__ void __launch_bounds__(256) k_res_apply(PrepArgs P) {
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(128) k_br_targets(LearnBufs LB, const float* __restrict__ tw, int a,
                                                     int64_t u0, int B, int E, double gamma,
-                                                    unsigned quirks) {
+                                                    unsigned quirks, int64_t it0, double lr0) {
   __shared__ __attribute__((aligned(16))) float sw[NET_LDS];
   __shared__ float q[MAX_BATCH][3];
   __shared__ float val[MAX_BATCH];
@@ -273,15 +297,20 @@ __global__ void __launch_bounds__(128) k_br_targets(LearnBufs LB, const float* _
     q[b][am[b]] = val[b];
   }
   __syncthreads();
-  if (b < B) {
-    for (int e = 0; e < E; ++e) {
+  for (int e = 0; e < E; ++e) {
+    uint32_t x = 0;
+    if (b < B) {
       const int k = LB.br_perm[(slot * E + e) * B + b];
       FitRow fr;
-      fr.x = sb[k];
+      fr.x = x = sb[k];
       fr.t0 = q[k][0]; fr.t1 = q[k][1]; fr.t2 = q[k][2];
       LB.br_fit[(slot * E + e) * B + b] = fr;
     }
+    emit_xt(LB.br_xt + (slot * E + e) * B, x, B);
   }
+  // lr of this update: lr0 / (1 + 0.003 sqrt(iteration)) with iteration = it0 + 2 u
+  // (agent/agent.py:249, iteration += 2 per BR update), in the reference's double arithmetic
+  if (b == 0) LB.br_lr[slot] = (float)(lr0 / (1.0 + 0.003 * sqrt((double)(it0 + 2 * u))));
 }
 
 // ---------------------------------------------------------------------------
@@ -304,6 +333,8 @@ struct ChainArgs {
   double lr0;                     // BR: lr_u = lr0 / (1 + 0.003 sqrt(it0 + 2u))
   int64_t it0[2];
   unsigned long long* stamps;     // diagnostic build only (NFSP_CHAIN_STAMPS): phase cycles
+  const uint32_t* xt;             // k_chain3: bit-transposed minibatch masks, fit's layout
+  const float* lr_tab;            // k_chain3 BR: [2][umax] per-update lr
 };
 
 // In-kernel phase stamps (cdna_hip_programming.md §7): a separate diagnostic build only.
@@ -927,6 +958,358 @@ __global__ void __launch_bounds__(256) k_chain2(ChainArgs C) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// k_chain3: the SGD chain on bf16 matrix cores with exact-f32 operands.
+//
+// An f32 value v is split exactly into three bf16 terms v = hi + mid + lo (8 + 8 + 8
+// significand bits, round-to-nearest at each cut), and a Leduc observation is 0/1, so
+// X.W = X.lo + X.mid + X.hi with every product exact and f32 accumulation: the 16 chained
+// v_mfma_f32_16x16x4_f32 of a layer-1 product become 6 v_mfma_f32_16x16x32_bf16 (K = 32
+// covers all 30 inputs).  Per wave (hidden slice 16w..16w+15, lane (g, c) = (l >> 4, l & 15)):
+//   * layer-1 K slot 8g + j <-> input pi(g, j) = 4g + j (j < 4) or 16 + 4g + j - 4, so the
+//     dW1 accumulator lands in the registers that hold W1 (wr[j] = W1[pi(g, j)][16w + c]);
+//   * forward twice from the same registers: Z1 sample-major (D row = sample, for the
+//     backward and dW1) and Z1^T hidden-major (D row = hidden: layer 2 is then 4 lane-local
+//     FMAs per output plus two permlane swaps instead of a 16-lane reduction);
+//   * dW1 = X^T dZ1 with K = samples: the A operand comes from the bit-transposed masks
+//     (xt) the prep kernels emit, the B operand is dZ1 split the same way;
+//   * operands of step t+1 are formed during step t from rows loaded two steps ahead
+//     (two named buffers, loop unrolled by two: no load result is ever copied);
+//   * one barrier per step (the 4 waves' layer-2 partials), all other exchange is
+//     wave-private (LDS dm / w2t) or cross-lane (DPP, permlane).
+// ---------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+
+struct Chain3Smem {
+  float po[2][4][32][4];     // per-wave partial layer-2 outputs, double-buffered by step parity
+  float dm[4][3][32];        // wave-private: dL/dz2 of the 32 samples, by output
+  float4 w2t[4][16];         // wave-private: (W2[h][0..2], b1[h]) of the slice, for Z1^T
+};
+
+// 8 bf16 0/1 values of the K slots 8g..8g+7 from a 32-bit mask: bits 4g..4g+3, 16+4g..+3
+__device__ inline bf16x8 bits8(uint32_t x, int g) {
+  const uint32_t n0 = (x >> (4 * g)) & 0xFu, n1 = (x >> (16 + 4 * g)) & 0xFu;
+  u32x4v r;
+  r[0] = (n0 & 1u) * 0x3F80u + ((n0 >> 1) & 1u) * 0x3F800000u;
+  r[1] = ((n0 >> 2) & 1u) * 0x3F80u + ((n0 >> 3) & 1u) * 0x3F800000u;
+  r[2] = (n1 & 1u) * 0x3F80u + ((n1 >> 1) & 1u) * 0x3F800000u;
+  r[3] = ((n1 >> 2) & 1u) * 0x3F80u + ((n1 >> 3) & 1u) * 0x3F800000u;
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+// exact three-term bf16 split of 8 f32 values
+__device__ inline void split3(const float (&v)[8], bf16x8& hi, bf16x8& mid, bf16x8& lo) {
+#pragma clang fp contract(off)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 h = (__bf16)v[j];
+    const float r1 = v[j] - (float)h;
+    const __bf16 m = (__bf16)r1;
+    const float r2 = r1 - (float)m;
+    hi[j] = h;
+    mid[j] = m;
+    lo[j] = (__bf16)r2;
+  }
+}
+
+__device__ inline floatx4 mfma3(bf16x8 a, bf16x8 bhi, bf16x8 bmid, bf16x8 blo) {
+  floatx4 z = {};
+  z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, blo, z, 0, 0, 0);
+  z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bmid, z, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bhi, z, 0, 0, 0);
+}
+__device__ inline floatx4 mfma3t(bf16x8 ahi, bf16x8 amid, bf16x8 alo, bf16x8 b) {
+  floatx4 z = {};
+  z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo, b, z, 0, 0, 0);
+  z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(amid, b, z, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, b, z, 0, 0, 0);
+}
+
+struct C3Buf {               // one step's loads (lane-specific)
+  uint4 ra, rb;              // fit rows c and 16 + c: (x, t0, t1, t2)
+  uint32_t xa, xb;           // xt words c and 16 + c
+  float lr;
+};
+struct C3Ops {               // one step's operands, formed a step ahead
+  bf16x8 fa0, fa1;           // X bits of samples c / 16 + c (Z1 A operand, Z1^T B operand)
+  bf16x8 ba0, ba1;           // X^T bits of inputs c / 16 + c over the samples (dW1 A operand)
+  float t0, t1, t2;          // fit targets of this lane's loss sample 16 (g >> 1) + c
+  float lr;
+};
+
+template <int RELU>
+__global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  Chain3Smem& sm = *reinterpret_cast<Chain3Smem*>(smem_raw);
+  const int a = C.agents[blockIdx.x];
+  const int tid = threadIdx.x;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l = tid & 63;
+  const int g = l >> 4, c = l & 15;
+  const int hid = 16 * w + c;
+  const int sl = 16 * (g >> 1) + c;            // this lane's loss sample
+  float* gw = C.w[blockIdx.x];
+  float wr[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int i = 16 * (j >> 2) + 4 * g + (j & 3);
+    wr[j] = i < nfsp::OBS ? gw[nn::OW1 + i * nn::H + hid] : 0.f;
+  }
+  float b1 = gw[nn::OB1 + hid];
+  float W2_0 = gw[nn::OW2 + 3 * hid + 0], W2_1 = gw[nn::OW2 + 3 * hid + 1], W2_2 = gw[nn::OW2 + 3 * hid + 2];
+  float b2_0 = gw[nn::OB2 + 0], b2_1 = gw[nn::OB2 + 1], b2_2 = gw[nn::OB2 + 2];
+  const int nmb = C.B / CHAIN_MB;
+  const int spu = C.E * nmb;                   // SGD steps per update
+  const float inv3m = 1.0f / (float)(3 * CHAIN_MB);
+  const float invm = 1.0f / (float)CHAIN_MB;
+  const int64_t slot0 = (int64_t)a * C.umax;
+  const int64_t u1 = C.u1[blockIdx.x];
+  int64_t u0 = C.u0[blockIdx.x];
+  if (C.active) {          // AR: skip the inactive prefix (M_SL <= batch; monotone in u)
+    while (u0 < u1) {
+      const int64_t q = u0 + l;
+      const unsigned long long m = __ballot(q < u1 && C.active[slot0 + q]);
+      if (m) { u0 += __builtin_ctzll(m); break; }
+      u0 += 64;
+    }
+    if (u0 > u1) u0 = u1;
+  }
+  const int T1 = (int)(u1 * spu);
+  int t = (int)(u0 * spu);
+  const uint4* fitb = reinterpret_cast<const uint4*>(C.fit + slot0 * C.E * C.B);
+  const uint32_t* xtb = C.xt + slot0 * C.E * C.B;
+  const float* lrb = RELU ? C.lr_tab + slot0 : nullptr;
+  // loader position (the step whose rows the next load_next fetches) and its update
+  int lpos = t, lu = (int)u0, lk = 0;
+  auto load_next = [&](C3Buf& b) {
+    const int p = lpos < T1 ? lpos : T1 - 1;
+    b.ra = fitb[32 * p + c];
+    b.rb = fitb[32 * p + 16 + c];
+    b.xa = xtb[32 * p + c];
+    b.xb = xtb[32 * p + 16 + c];
+    b.lr = RELU ? lrb[lu < u1 ? lu : u1 - 1] : C.lr_fixed;
+    ++lpos;
+    if (++lk == spu) { lk = 0; ++lu; }
+  };
+  auto make_ops = [&](C3Ops& o, const C3Buf& b) {
+    o.fa0 = bits8(b.ra.x, g);
+    o.fa1 = bits8(b.rb.x, g);
+    o.ba0 = bits8(b.xa, g);
+    o.ba1 = bits8(b.xb, g);
+    const uint4 tr = (g >> 1) ? b.rb : b.ra;
+    o.t0 = __uint_as_float(tr.y);
+    o.t1 = __uint_as_float(tr.z);
+    o.t2 = __uint_as_float(tr.w);
+    o.lr = b.lr;
+  };
+  auto publish = [&]() {   // this wave's (W2, b1) rows for its own Z1^T layer 2
+    if (g == 0) sm.w2t[w][c] = make_float4(W2_0, W2_1, W2_2, b1);
+  };
+#ifdef NFSP_CHAIN_STAMPS
+  unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_last = 0;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
+#endif
+  auto step = [&](const C3Ops& o, C3Buf& mine, C3Ops& nxt, const C3Buf& other) {
+    load_next(mine);                               // rows of step t + 2
+    // ---- layer 1, both orientations
+    bf16x8 whi, wmid, wlo;
+    split3(wr, whi, wmid, wlo);
+    float W2h[4][3], b1h[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float4 q = sm.w2t[w][4 * g + r];
+      W2h[r][0] = q.x; W2h[r][1] = q.y; W2h[r][2] = q.z; b1h[r] = q.w;
+    }
+    const floatx4 zh0 = mfma3t(whi, wmid, wlo, o.fa0);   // Z1^T: hidden 16w+4g+r, sample c
+    const floatx4 zh1 = mfma3t(whi, wmid, wlo, o.fa1);   //                      sample 16+c
+    const floatx4 zs0 = mfma3(o.fa0, whi, wmid, wlo);    // Z1: sample 4g+r, hidden 16w+c
+    const floatx4 zs1 = mfma3(o.fa1, whi, wmid, wlo);    //     sample 16+4g+r
+    CHAIN_STAMP(0);
+    // ---- layer 2 partial over the slice, from Z1^T
+    float p0[3], p1[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { p0[k] = 0.f; p1[k] = 0.f; }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float h0 = fmaxf(zh0[r] + b1h[r], 0.f);
+      const float h1 = fmaxf(zh1[r] + b1h[r], 0.f);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        p0[k] = p0[k] + h0 * W2h[r][k];
+        p1[k] = p1[k] + h1 * W2h[r][k];
+      }
+    }
+    float q[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {   // rows g, g ^ 2 (tile halves), then g ^ 1
+      const auto rr = __builtin_amdgcn_permlane32_swap(__float_as_uint(p0[k]), __float_as_uint(p1[k]),
+                                                       false, false);
+      q[k] = sum_x16(__uint_as_float(rr[0]) + __uint_as_float(rr[1]));
+    }
+    const int buf = t & 1;
+    if ((g & 1) == 0) *reinterpret_cast<float4*>(&sm.po[buf][w][sl][0]) = make_float4(q[0], q[1], q[2], 0.f);
+    CHAIN_STAMP(1);
+    __syncthreads();
+    CHAIN_STAMP(2);
+    // ---- output + loss of sample sl (every wave redundantly, identical results)
+    float d0, d1, d2;
+    {
+      const float4 a0 = *reinterpret_cast<const float4*>(&sm.po[buf][0][sl][0]);
+      const float4 a1 = *reinterpret_cast<const float4*>(&sm.po[buf][1][sl][0]);
+      const float4 a2 = *reinterpret_cast<const float4*>(&sm.po[buf][2][sl][0]);
+      const float4 a3 = *reinterpret_cast<const float4*>(&sm.po[buf][3][sl][0]);
+      const float o0 = (((a0.x + a1.x) + a2.x) + a3.x) + b2_0;
+      const float o1 = (((a0.y + a1.y) + a2.y) + a3.y) + b2_1;
+      const float o2 = (((a0.z + a1.z) + a2.z) + a3.z) + b2_2;
+      const float tt[3] = {o.t0, o.t1, o.t2};
+      if (RELU) {          // Huber on ReLU outputs, mean over 3 x batch
+        const float oz[3] = {o0, o1, o2};
+        float dd[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const float y = oz[k] > 0.f ? oz[k] : 0.f;
+          const float ee = tt[k] - y;
+          const float gg = fabsf(ee) > 1.0f ? (ee > 0.f ? 1.f : -1.f) : ee;
+          dd[k] = oz[k] > 0.f ? (-gg * inv3m) : 0.f;
+        }
+        d0 = dd[0]; d1 = dd[1]; d2 = dd[2];
+      } else {             // Keras categorical cross-entropy on softmax (normalise + clip)
+        const float mx = fmaxf(fmaxf(o0, o1), o2);
+        const float e0 = __expf(o0 - mx), e1 = __expf(o1 - mx), e2 = __expf(o2 - mx);
+        const float rs = __builtin_amdgcn_rcpf((e0 + e1) + e2);
+        const float y[3] = {e0 * rs, e1 * rs, e2 * rs};
+        const float S = (y[0] + y[1]) + y[2];
+        const float rS = __builtin_amdgcn_rcpf(S);
+        const float eps = 1e-7f, hi = 1.0f - 1e-7f;
+        float dp[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const float pk = y[k] * rS;
+          const float pc = fminf(fmaxf(pk, eps), hi);
+          const float msk = (pk >= eps && pk <= hi) ? invm : 0.f;
+          dp[k] = -(tt[k] * __builtin_amdgcn_rcpf(pc)) * msk;
+        }
+        const float dpy = (dp[0] * y[0] + dp[1] * y[1]) + dp[2] * y[2];
+        float dy[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) dy[k] = (dp[k] - dpy * rS) * rS;
+        const float dyy = (dy[0] * y[0] + dy[1] * y[1]) + dy[2] * y[2];
+        d0 = y[0] * (dy[0] - dyy);
+        d1 = y[1] * (dy[1] - dyy);
+        d2 = y[2] * (dy[2] - dyy);
+      }
+    }
+    if ((g & 1) == 0) {
+      sm.dm[w][0][sl] = d0;
+      sm.dm[w][1][sl] = d1;
+      sm.dm[w][2][sl] = d2;
+    }
+    float gb2[3] = {d0, d1, d2};     // sum over the 32 samples: the row's 16, then rows g ^ 2
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      float x = gb2[k];
+      x = x + dpp_any(x, 0x128);
+      x = x + dpp_any(x, 0x124);
+      x = x + dpp_any(x, 0x122);
+      x = x + dpp_any(x, 0x121);
+      gb2[k] = sum_x32(x);
+    }
+    CHAIN_STAMP(3);
+    // ---- backward in the sample-major layout: samples 16 mt + 4g + r, hidden 16w + c
+    float4 dA[3], dB[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      dA[k] = *reinterpret_cast<const float4*>(&sm.dm[w][k][4 * g]);
+      dB[k] = *reinterpret_cast<const float4*>(&sm.dm[w][k][16 + 4 * g]);
+    }
+    float dz[8];
+    float g2_0 = 0.f, g2_1 = 0.f, g2_2 = 0.f, gb1 = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int r = j & 3;
+      const float z = (j < 4 ? zs0[r] : zs1[r]) + b1;
+      const float4 e0 = j < 4 ? dA[0] : dB[0], e1 = j < 4 ? dA[1] : dB[1], e2 = j < 4 ? dA[2] : dB[2];
+      const float x0 = r == 0 ? e0.x : r == 1 ? e0.y : r == 2 ? e0.z : e0.w;
+      const float x1 = r == 0 ? e1.x : r == 1 ? e1.y : r == 2 ? e1.z : e1.w;
+      const float x2 = r == 0 ? e2.x : r == 1 ? e2.y : r == 2 ? e2.z : e2.w;
+      const float h = z > 0.f ? z : 0.f;
+      g2_0 += h * x0;
+      g2_1 += h * x1;
+      g2_2 += h * x2;
+      const float dh = (x0 * W2_0 + x1 * W2_1) + x2 * W2_2;
+      dz[j] = z > 0.f ? dh : 0.f;
+      gb1 += dz[j];
+    }
+    bf16x8 dhi, dmid, dlo;
+    split3(dz, dhi, dmid, dlo);
+    // dW1[16 it + 4g + r][16w + c] = sum over the 32 samples (K slot 8g + j <-> sample
+    // 16 (j >> 2) + 4g + (j & 3), the order of dz)
+    const floatx4 gA = mfma3(o.ba0, dhi, dmid, dlo);
+    const floatx4 gB = mfma3(o.ba1, dhi, dmid, dlo);
+    g2_0 = sum_x16(sum_x32(g2_0));
+    g2_1 = sum_x16(sum_x32(g2_1));
+    g2_2 = sum_x16(sum_x32(g2_2));
+    gb1 = sum_x16(sum_x32(gb1));
+    CHAIN_STAMP(4);
+    const float lr = o.lr;
+    W2_0 = W2_0 - lr * g2_0;
+    W2_1 = W2_1 - lr * g2_1;
+    W2_2 = W2_2 - lr * g2_2;
+    b1 = b1 - lr * gb1;
+    b2_0 = b2_0 - lr * gb2[0];
+    b2_1 = b2_1 - lr * gb2[1];
+    b2_2 = b2_2 - lr * gb2[2];
+    publish();
+    make_ops(nxt, other);                          // operands of step t + 1
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      wr[r] = wr[r] - lr * gA[r];
+      wr[4 + r] = wr[4 + r] - lr * gB[r];
+    }
+    CHAIN_STAMP(5);
+  };
+  if (t < T1) {
+    C3Buf bA, bB;
+    C3Ops oA, oB;
+    load_next(bA);
+    load_next(bB);
+    make_ops(oA, bA);
+    publish();
+    for (;;) {
+      step(oA, bA, oB, bB);
+      if (++t >= T1) break;
+      step(oB, bB, oA, bA);
+      if (++t >= T1) break;
+    }
+  }
+#ifdef NFSP_CHAIN_STAMPS
+  if (C.stamps && l == 0)
+    for (int k = 0; k < 10; ++k) C.stamps[(blockIdx.x * 4 + w) * 10 + k] = st_acc[k];
+#endif
+  float* dsts[2] = {gw, C.sync_to[blockIdx.x]};
+  for (int k = 0; k < 2; ++k) {
+    float* dst = dsts[k];
+    if (!dst) continue;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = 16 * (j >> 2) + 4 * g + (j & 3);
+      if (i < nfsp::OBS) dst[nn::OW1 + i * nn::H + hid] = wr[j];
+    }
+    if (g == 0) {
+      dst[nn::OB1 + hid] = b1;
+      dst[nn::OW2 + 3 * hid + 0] = W2_0;
+      dst[nn::OW2 + 3 * hid + 1] = W2_1;
+      dst[nn::OW2 + 3 * hid + 2] = W2_2;
+    }
+    if (w == 0 && l == 0) {
+      dst[nn::OB2 + 0] = b2_0;
+      dst[nn::OB2 + 1] = b2_1;
+      dst[nn::OB2 + 2] = b2_2;
+    }
+  }
+}
+
 // schedule state after the learner (host-computed values + device-side counters)
 struct FinalArgs {
   EngineDev* st;
@@ -1037,6 +1420,7 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
     NFSP_HIP(hipStreamWaitEvent(e->s_ar, fork, 0));
     ChainArgs C{};
     C.fit = e->LB.ar_fit;
+    C.xt = e->LB.ar_xt;
     C.active = e->LB.ar_active;
     C.umax = e->LB.umax;
     C.B = cfg.batch;
@@ -1051,7 +1435,7 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
       C.u1[a] = P.A[a].U;
     }
     KTimer kc(e, KT_CHAIN_AR, e->s_ar);
-    k_chain2<0><<<2, 256, sizeof(Chain2Smem), e->s_ar>>>(C);
+    k_chain3<0><<<2, 256, sizeof(Chain3Smem), e->s_ar>>>(C);
     NFSP_LAUNCHED("k_chain(AR)");
   }
   // ---- BR: per agent, segments between target syncs, each = targets + chain
@@ -1085,11 +1469,13 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
       {
         KTimer kt2(e, KT_TARGETS, sa);
         k_br_targets<<<(unsigned)(v - u), 128, 0, sa>>>(e->LB, wtg, a, u, cfg.batch, cfg.epochs,
-                                                         cfg.gamma, cfg.quirks);
+                                                         cfg.gamma, cfg.quirks, it0, cfg.lr_br);
       }
       NFSP_LAUNCHED("k_br_targets");
       ChainArgs C{};
       C.fit = e->LB.br_fit;
+      C.xt = e->LB.br_xt;
+      C.lr_tab = e->LB.br_lr;
       C.active = nullptr;
       C.umax = e->LB.umax;
       C.B = cfg.batch;
@@ -1104,7 +1490,7 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
       C.it0[0] = it0;
       {
         KTimer kc(e, KT_CHAIN_BR, sa);
-        k_chain2<1><<<1, 256, sizeof(Chain2Smem), sa>>>(C);
+        k_chain3<1><<<1, 256, sizeof(Chain3Smem), sa>>>(C);
       }
       NFSP_LAUNCHED("k_chain(BR)");
       u = v;
