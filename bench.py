@@ -167,8 +167,8 @@ def main():
         return {"kernel": name, "bound": "mfma", "achieved": ach, "peak": PEAK_FP32_TFLOPS,
                 "unit": "TFLOP/s", "frac": ach / PEAK_FP32_TFLOPS, "traffic": None,
                 "avg_ms": k_ms[name], "launches": k_launches[name], "flop_per_launch": flop}
-    roofs = {"k_chain2_br": chain_roof("k_chain2_br", br_upd),
-             "k_chain2_ar": chain_roof("k_chain2_ar", ar_upd),
+    roofs = {"k_chain3_br": chain_roof("k_chain3_br", br_upd),
+             "k_chain3_ar": chain_roof("k_chain3_ar", ar_upd),
              "k_rollout": roof_rollout}
     # the dominant kernel = largest GPU time inside the timed region
     singles = [k for k in timings if k != "learner"]

@@ -440,12 +440,9 @@ extern "C" int nfsp_engine_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, nfs
   EALLOC(L.br_rows, sizeof(BrRow) * ub);
   EALLOC(L.br_perm, ueb);
   EALLOC(L.br_expl, sizeof(double) * 2 * L.umax);
-  EALLOC(L.br_fit, sizeof(FitRow) * ueb);
-  EALLOC(L.ar_fit, sizeof(FitRow) * ueb);
+  EALLOC(L.br_rec, sizeof(StepRec) * (ueb / CHAIN_MB));
+  EALLOC(L.ar_rec, sizeof(StepRec) * (ueb / CHAIN_MB));
   EALLOC(L.ar_active, 2 * L.umax);
-  EALLOC(L.br_xt, 4 * ueb);
-  EALLOC(L.ar_xt, 4 * ueb);
-  EALLOC(L.br_lr, 4 * 2 * L.umax);
   EALLOC(L.res_head, sizeof(unsigned long long) * sc);
   EALLOC(L.res_next, 4 * pc);
   EALLOC(L.res_slot, 4 * pc);

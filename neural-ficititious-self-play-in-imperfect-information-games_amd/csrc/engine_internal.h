@@ -69,10 +69,17 @@ struct Memories {
   int32_t* dbg_perms;   // [4][epochs][batch]
 };
 
-// One prepared minibatch row of an SGD chain: observation bits + 3 fit targets.
-struct __attribute__((aligned(16))) FitRow {
-  uint32_t x;
-  float t0, t1, t2;
+// Everything one SGD step of a learner chain (learner.hip k_chain3) reads, built by the
+// prep kernels so the chain's lanes load their matrix-core operands directly:
+//   fa[g][s]  8 bf16 0/1 values: bits 4g..4g+3 and 16+4g..16+4g+3 of sample s's observation
+//             (the layer-1 K slots 8g..8g+7 of lane row g)
+//   ba[g][i]  the same bits of input i's 32-bit mask over the minibatch's 32 samples (the
+//             bit-transposed minibatch: the dW1 = X^T dZ1 operand)
+//   tg[s]     sample s's three fit targets and the step's learning rate
+struct __attribute__((aligned(16))) StepRec {
+  uint4 fa[4][32];
+  uint4 ba[4][32];
+  float4 tg[32];
 };
 
 // A sampled M_RL row before its TD target exists.
@@ -86,11 +93,8 @@ struct LearnBufs {
   BrRow* br_rows;      // [2][umax][batch]
   uint8_t* br_perm;    // [2][umax][epochs][batch]
   double* br_expl;     // [2][umax]
-  FitRow* br_fit;      // [2][umax][epochs][batch]
-  FitRow* ar_fit;      // [2][umax][epochs][batch]
-  uint32_t* br_xt;     // [2][umax][epochs][batch / 32][32]: per minibatch, the mask over its
-  uint32_t* ar_xt;     //   32 samples of every input (bit-transposed x), the dW1 operand
-  float* br_lr;        // [2][umax] per-update BR learning rate (agent/agent.py:249)
+  StepRec* br_rec;     // [2][umax][epochs][batch / 32]: one record per SGD step
+  StepRec* ar_rec;     // [2][umax][epochs][batch / 32]
   uint8_t* ar_active;  // [2][umax]
   unsigned long long* res_head;   // [2][sl_cap]  (tag << 32 | q)
   int32_t* res_next;   // [2][pend_cap]

@@ -15,7 +15,7 @@
 //                                     slot contents AS OF the trigger, perms -> fit rows
 //   k_res_apply     [all SL inserts]  final reservoir contents (last writer per slot)
 //   k_br_targets    [a segment]       Q_target forwards, TD values, proxy, row-0 quirk
-//   k_chain<BR/AR>  [1 WG per agent]  epochs x minibatch SGD, weights in LDS/registers
+//   k_chain3<BR/AR> [1 WG per agent]  epochs x minibatch SGD, whole net in registers
 // BR chains are cut into segments at target-sync points; the two agents' BR chains and
 // the AR chains run on separate streams.
 #include <math.h>
@@ -46,6 +46,7 @@ struct PrepArgs {
   int64_t c, rl_cap;
   int B, E;
   uint32_t k0, k1, tag;
+  float lr_ar;
 };
 
 __device__ inline uint32_t row_bits(const float* __restrict__ r) {
@@ -124,22 +125,45 @@ __global__ void __launch_bounds__(256) k_ar_slots(PrepArgs P) {
   }
 }
 
-// Bit-transposed minibatch masks for the chain's dW1 operand: thread b holds the mask of
-// fit position b of one (update, epoch) block (0 for b >= B); writes xt[mb][i] = bit i of
-// the masks of minibatch mb's 32 rows (bit k = row 32 mb + k).  Whole block (a multiple of
-// 64 threads) calls.
-__device__ inline void emit_xt(uint32_t* __restrict__ xt, uint32_t x, int B) {
-  const int lane = threadIdx.x & 63;
+// 8 bf16 0/1 values of the layer-1 K slots 8g..8g+7 (bits 4g..4g+3, 16+4g..16+4g+3 of x)
+__device__ inline uint4 bits8u(uint32_t x, int g) {
+  const uint32_t n0 = (x >> (4 * g)) & 0xFu, n1 = (x >> (16 + 4 * g)) & 0xFu;
+  return make_uint4((n0 & 1u) * 0x3F80u + ((n0 >> 1) & 1u) * 0x3F800000u,
+                    ((n0 >> 2) & 1u) * 0x3F80u + ((n0 >> 3) & 1u) * 0x3F800000u,
+                    (n1 & 1u) * 0x3F80u + ((n1 >> 1) & 1u) * 0x3F800000u,
+                    ((n1 >> 2) & 1u) * 0x3F80u + ((n1 >> 3) & 1u) * 0x3F800000u);
+}
+
+// The chain records of one (update, epoch): thread b holds fit position b's observation
+// mask x (0 for b >= B), targets and the lr; minibatch b >> 5 gets fa / tg of its sample
+// b & 31, and ba from the bit transpose of its 32 masks by wave ballot.  Whole block (a
+// multiple of 64 threads) calls.
+__device__ inline void emit_recs(StepRec* __restrict__ recs, uint32_t x, float t0, float t1, float t2,
+                                 float lr, int B) {
+  const int b = threadIdx.x;
+  if (b < B) {
+    StepRec& R = recs[b >> 5];
+    const int k = b & 31;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) R.fa[g][k] = bits8u(x, g);
+    R.tg[k] = make_float4(t0, t1, t2, lr);
+  }
+  const int lane = b & 63;
   unsigned long long mine = 0;
 #pragma unroll
   for (int i = 0; i < nfsp::OBS; ++i) {
     const unsigned long long m = __ballot((x >> i) & 1u);
     if (lane == i) mine = m;
   }
-  const int mb = (threadIdx.x >> 6) * 2;
+  const int mb = (b >> 6) * 2;          // this wave's two minibatches
   if (lane < 32) {
-    if (32 * mb < B) xt[mb * 32 + lane] = (uint32_t)mine;
-    if (32 * (mb + 1) < B) xt[(mb + 1) * 32 + lane] = (uint32_t)(mine >> 32);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (32 * (mb + h) >= B) continue;
+      const uint32_t xt = (uint32_t)(mine >> (32 * h));
+#pragma unroll
+      for (int g = 0; g < 4; ++g) recs[mb + h].ba[g][lane] = bits8u(xt, g);
+    }
   }
 }
 
@@ -166,6 +190,7 @@ __global__ void __launch_bounds__(128) k_ar_prep(PrepArgs P) {
   __shared__ uint32_t rx[MAX_BATCH];
   __shared__ float ra[MAX_BATCH][3];
   __shared__ uint32_t px[MAX_BATCH];
+  __shared__ float pt[MAX_BATCH][3];
   __shared__ int64_t s_nb;
   const int a = blockIdx.y;
   const int64_t u = blockIdx.x;
@@ -219,16 +244,15 @@ __global__ void __launch_bounds__(128) k_ar_prep(PrepArgs P) {
   for (int e = 0; e < P.E; ++e) {
     int rank;
     draw_perm(key, P.B, e, TAG_PERM | (uint32_t)dbg, m, P.k0, P.k1, rank);
-    if (b < P.B) {
-      FitRow fr;
-      fr.x = rx[b];
-      fr.t0 = ra[b][0]; fr.t1 = ra[b][1]; fr.t2 = ra[b][2];
-      P.LB.ar_fit[(slot_u * P.E + e) * P.B + rank] = fr;
-      px[rank] = fr.x;
+    if (b < P.B) {        // fit position rank <- sampled row b
+      px[rank] = rx[b];
+      pt[rank][0] = ra[b][0]; pt[rank][1] = ra[b][1]; pt[rank][2] = ra[b][2];
       if (last) P.M.dbg_perms[(dbg * P.E + e) * P.B + rank] = b;
     }
     __syncthreads();
-    emit_xt(P.LB.ar_xt + (slot_u * P.E + e) * P.B, b < P.B ? px[b] : 0u, P.B);
+    const bool in = b < P.B;
+    emit_recs(P.LB.ar_rec + (slot_u * P.E + e) * (P.B / CHAIN_MB), in ? px[b] : 0u, in ? pt[b][0] : 0.f,
+              in ? pt[b][1] : 0.f, in ? pt[b][2] : 0.f, P.lr_ar, P.B);
     __syncthreads();
   }
   if (last && b < P.B) P.M.dbg_rows[dbg * P.B + b] = cand[b];
@@ -297,44 +321,36 @@ __global__ void __launch_bounds__(128) k_br_targets(LearnBufs LB, const float* _
     q[b][am[b]] = val[b];
   }
   __syncthreads();
-  for (int e = 0; e < E; ++e) {
-    uint32_t x = 0;
-    if (b < B) {
-      const int k = LB.br_perm[(slot * E + e) * B + b];
-      FitRow fr;
-      fr.x = x = sb[k];
-      fr.t0 = q[k][0]; fr.t1 = q[k][1]; fr.t2 = q[k][2];
-      LB.br_fit[(slot * E + e) * B + b] = fr;
-    }
-    emit_xt(LB.br_xt + (slot * E + e) * B, x, B);
-  }
   // lr of this update: lr0 / (1 + 0.003 sqrt(iteration)) with iteration = it0 + 2 u
   // (agent/agent.py:249, iteration += 2 per BR update), in the reference's double arithmetic
-  if (b == 0) LB.br_lr[slot] = (float)(lr0 / (1.0 + 0.003 * sqrt((double)(it0 + 2 * u))));
+  const float lr = (float)(lr0 / (1.0 + 0.003 * sqrt((double)(it0 + 2 * u))));
+  for (int e = 0; e < E; ++e) {
+    uint32_t x = 0;
+    float t0 = 0.f, t1 = 0.f, t2 = 0.f;
+    if (b < B) {
+      const int k = LB.br_perm[(slot * E + e) * B + b];
+      x = sb[k];
+      t0 = q[k][0]; t1 = q[k][1]; t2 = q[k][2];
+    }
+    emit_recs(LB.br_rec + (slot * E + e) * (B / CHAIN_MB), x, t0, t1, t2, lr, B);
+  }
 }
 
 // ---------------------------------------------------------------------------
-// SGD chain: one workgroup (4 waves) per agent runs its updates back to back.
-// Wave w owns samples 8w..8w+7 of every 32-row minibatch, lane j owns hidden unit j.
-// W1 lives once in LDS; b1, W2 (per lane) and b2 are replicated in registers of every
-// wave and updated identically.  Minibatch rows are wave-uniform (scalar registers).
+// SGD chains: one workgroup (4 waves) per (agent, net) runs that net's updates back to
+// back with the whole net in registers (k_chain3).  Reference: agent/agent.py:241-264
+// (model.fit(batch_size=32, epochs=2) of the BR Q-net and the AR policy net).
 // ---------------------------------------------------------------------------
 struct ChainArgs {
   float* w[2];                    // weights of (agent, net)
   float* sync_to[2];              // BR: target net to copy into at the end (or null)
-  const FitRow* fit;              // [2][umax][E][B]
-  const uint8_t* active;          // AR: per-update flag (null for BR)
+  const StepRec* rec;             // [2][umax][E][B / 32] step records (prep kernels)
+  const uint8_t* active;          // AR: per-update flag, 0..0 1..1 in u (null for BR)
   int64_t umax;
   int64_t u0[2], u1[2];           // update range per agent
   int agents[2];                  // blockIdx -> agent
   int B, E;
-  int relu;                       // 1: BR (Huber), 0: AR (cross-entropy)
-  float lr_fixed;                 // AR lr
-  double lr0;                     // BR: lr_u = lr0 / (1 + 0.003 sqrt(it0 + 2u))
-  int64_t it0[2];
   unsigned long long* stamps;     // diagnostic build only (NFSP_CHAIN_STAMPS): phase cycles
-  const uint32_t* xt;             // k_chain3: bit-transposed minibatch masks, fit's layout
-  const float* lr_tab;            // k_chain3 BR: [2][umax] per-update lr
 };
 
 // In-kernel phase stamps (cdna_hip_programming.md §7): a separate diagnostic build only.
@@ -352,32 +368,7 @@ struct ChainArgs {
 #define CHAIN_STAMP(k) do { } while (0)
 #endif
 
-constexpr int ZROW = nfsp::OBS;            // an all-zero W1 row for padded gathers
-constexpr int W1ROWS = nfsp::OBS + 1;
-
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-
-struct ChainSmem {
-  float W1[W1ROWS * nn::H];
-  float gW1[4][nfsp::OBS * nn::H];     // per-wave partial W1 gradients (fully rewritten)
-  float gW2[4][nn::H * 3];
-  float gb1[4][nn::H];
-  float gb2[4][4];
-};
-
-// Wave-uniform W1 row offsets of the set bits of x (ascending), padded with the zero
-// row.  A Leduc observation has at most 9 set bits (<= 6 history + 3 card bits).
-__device__ inline void bit_rows(uint32_t x, int (&off)[9]) {
-#pragma unroll
-  for (int u = 0; u < 9; ++u) {
-    int i = ZROW;
-    if (x) {
-      i = __builtin_ctz(x);
-      x &= x - 1;
-    }
-    off[u] = i * nn::H;
-  }
-}
+typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 __device__ inline float dpp_f(float x, int ctrl) {
   switch (ctrl) {   // the control word must be an immediate
@@ -387,315 +378,6 @@ __device__ inline float dpp_f(float x, int ctrl) {
     default: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x141, 0xF, 0xF, false));
   }
 }
-
-// Sum over the 64 lanes of 24 values, halving the live values at every exchange so the
-// whole reduction is 42 cross-lane VALU ops and no LDS traffic:
-//   v_permlane32_swap (lanes 32-63 <-> 0-31):  24 values -> 12 per lane
-//   v_permlane16_swap (odd <-> even 16-rows):  12 -> 6
-//   DPP row_ror:8 (= lane ^ 8 within a row):    6 -> 3
-//   DPP quad xor 1, quad xor 2, row_half_mirror: full sums inside each 8-lane group.
-// Afterwards lane l holds the sums of values 3(l >> 3) + {0, 1, 2}.
-__device__ inline void reduce24(float (&v)[24], float& s0, float& s1, float& s2) {
-  const int lane = threadIdx.x & 63;
-  float w12[12], w6[6], w3[3];
-#pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 12]),
-                                                    false, false);
-    w12[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-  }
-#pragma unroll
-  for (int i = 0; i < 6; ++i) {
-    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(w12[i]), __float_as_uint(w12[i + 6]),
-                                                    false, false);
-    w6[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-  }
-  const bool h3 = lane & 8;
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const float keep = h3 ? w6[i + 3] : w6[i];
-    const float send = h3 ? w6[i] : w6[i + 3];
-    w3[i] = keep + dpp_f(send, 0x128);
-  }
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    w3[i] = w3[i] + dpp_f(w3[i], 0xB1);
-    w3[i] = w3[i] + dpp_f(w3[i], 0x4E);
-    w3[i] = w3[i] + dpp_f(w3[i], 0x141);
-  }
-  s0 = w3[0]; s1 = w3[1]; s2 = w3[2];
-}
-
-__device__ inline int64_t next_active(const ChainArgs& C, int64_t slot0, int64_t u, int64_t u1) {
-  if (C.active)
-    while (u < u1 && !C.active[slot0 + u]) ++u;
-  return u;
-}
-
-__global__ void __launch_bounds__(256) k_chain(ChainArgs C) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  ChainSmem& sm = *reinterpret_cast<ChainSmem*>(smem_raw);
-  const int a = C.agents[blockIdx.x];
-  const int tid = threadIdx.x;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int j = tid & 63;
-  const int myr = j >> 3;            // the sample whose loss this lane's 8-lane group computes
-  float* gw = C.w[blockIdx.x];
-  for (int i = tid; i < W1ROWS * nn::H; i += 256) sm.W1[i] = i < nfsp::OBS * nn::H ? gw[i] : 0.f;
-  float b1 = gw[nn::OB1 + j];
-  float W2_0 = gw[nn::OW2 + 3 * j + 0], W2_1 = gw[nn::OW2 + 3 * j + 1], W2_2 = gw[nn::OW2 + 3 * j + 2];
-  float b2_0 = gw[nn::OB2 + 0], b2_1 = gw[nn::OB2 + 1], b2_2 = gw[nn::OB2 + 2];
-  __syncthreads();
-  const int nmb = C.B / CHAIN_MB;
-  const float inv3m = 1.0f / (float)(3 * CHAIN_MB);
-  const float invm = 1.0f / (float)CHAIN_MB;
-  const int64_t slot0 = (int64_t)a * C.umax;
-  const int64_t u1 = C.u1[blockIdx.x];
-  int64_t u = next_active(C, slot0, C.u0[blockIdx.x], u1);
-  int e = 0, s = 0;
-  // each lane prefetches (one step ahead) the row of ITS group's sample
-  uint4 pf = make_uint4(0, 0, 0, 0);
-  auto issue = [&](int64_t uu, int ee, int ss) {
-    const uint4* rows = reinterpret_cast<const uint4*>(C.fit + ((slot0 + uu) * C.E + ee) * C.B +
-                                                       ss * CHAIN_MB + w * 8);
-    pf = rows[myr];
-  };
-  if (u < u1) issue(u, e, s);
-  float lr = 0.f;
-#ifdef NFSP_CHAIN_STAMPS
-  unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_last = 0;
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
-#endif
-  while (u < u1) {
-    const uint32_t xs = pf.x;                       // my group's sample
-    const float tt0 = __uint_as_float(pf.y), tt1 = __uint_as_float(pf.z), tt2 = __uint_as_float(pf.w);
-    uint32_t xb[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) xb[r] = __builtin_amdgcn_readlane(xs, 8 * r);
-    CHAIN_STAMP(0);
-    if (e == 0 && s == 0)
-      lr = C.relu ? (float)(C.lr0 / (1.0 + 0.003 * sqrt((double)(C.it0[blockIdx.x] + 2 * u)))) : C.lr_fixed;
-    // advance (u, e, s) and prefetch the next step's row
-    int64_t nu = u;
-    int ne = e, ns = s + 1;
-    if (ns == nmb) {
-      ns = 0;
-      if (++ne == C.E) {
-        ne = 0;
-        nu = next_active(C, slot0, u + 1, u1);
-      }
-    }
-    if (nu < u1) issue(nu, ne, ns);
-    CHAIN_STAMP(1);
-    // ---- forward: padded, branch-free gathers of the set bits' W1 rows
-    float z1[8];
-    float v[24];
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      int off[4][9];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) bit_rows(xb[4 * hh + r], off[r]);
-      float wv[4][9];
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int q = 0; q < 9; ++q) wv[r][q] = sm.W1[off[r][q] + j];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float acc = 0.f;
-#pragma unroll
-        for (int q = 0; q < 9; ++q) acc = acc + wv[r][q];
-        const int rr = 4 * hh + r;
-        z1[rr] = acc + b1;
-        const float h = z1[rr] > 0.f ? z1[rr] : 0.f;
-        v[3 * rr + 0] = h * W2_0;
-        v[3 * rr + 1] = h * W2_1;
-        v[3 * rr + 2] = h * W2_2;
-      }
-    }
-    CHAIN_STAMP(2);
-    float s0, s1, s2;
-    reduce24(v, s0, s1, s2);          // lane group g now holds sample g's three sums
-    CHAIN_STAMP(3);
-    // ---- loss gradient of my group's sample, then broadcast all 8 samples' to SGPRs
-    float d0, d1, d2;
-    {
-      const float o0 = s0 + b2_0, o1 = s1 + b2_1, o2 = s2 + b2_2;
-      if (C.relu) {
-        const float zz[3] = {o0, o1, o2}, tt[3] = {tt0, tt1, tt2};
-        float dd[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          const float y = zz[k] > 0.f ? zz[k] : 0.f;
-          const float ee = tt[k] - y;
-          const float g = fabsf(ee) > 1.0f ? (ee > 0.f ? 1.f : (ee < 0.f ? -1.f : 0.f)) : ee;
-          dd[k] = zz[k] > 0.f ? (-g * inv3m) : 0.f;
-        }
-        d0 = dd[0]; d1 = dd[1]; d2 = dd[2];
-      } else {
-        const float mx = fmaxf(fmaxf(o0, o1), o2);
-        const float e0 = expf(o0 - mx), e1 = expf(o1 - mx), e2 = expf(o2 - mx);
-        const float ssum = (e0 + e1) + e2;
-        const float y[3] = {e0 / ssum, e1 / ssum, e2 / ssum};
-        const float S = (y[0] + y[1]) + y[2];
-        const float eps = 1e-7f, hi = 1.0f - 1e-7f;
-        const float tt[3] = {tt0, tt1, tt2};
-        float dp[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          const float p = y[k] / S;
-          const float pc = fminf(fmaxf(p, eps), hi);
-          const float msk = (p >= eps && p <= hi) ? 1.f : 0.f;
-          dp[k] = (-tt[k] / pc) * msk * invm;
-        }
-        const float dpy = (dp[0] * y[0] + dp[1] * y[1]) + dp[2] * y[2];
-        float dy[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) dy[k] = dp[k] / S - dpy / (S * S);
-        const float dyy = (dy[0] * y[0] + dy[1] * y[1]) + dy[2] * y[2];
-        d0 = y[0] * (dy[0] - dyy);
-        d1 = y[1] * (dy[1] - dyy);
-        d2 = y[2] * (dy[2] - dyy);
-      }
-    }
-    float dr[8][3];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      dr[r][0] = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(d0), 8 * r));
-      dr[r][1] = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(d1), 8 * r));
-      dr[r][2] = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(d2), 8 * r));
-    }
-    CHAIN_STAMP(4);
-    // ---- backward: layer 2 / biases on the VALU, W1 gradient (X^T dZ1) on MFMA
-    float g2_0 = 0.f, g2_1 = 0.f, g2_2 = 0.f, gb1 = 0.f, gb2_0 = 0.f, gb2_1 = 0.f, gb2_2 = 0.f;
-    float dz1[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const float h = z1[r] > 0.f ? z1[r] : 0.f;
-      g2_0 += h * dr[r][0];
-      g2_1 += h * dr[r][1];
-      g2_2 += h * dr[r][2];
-      gb2_0 += dr[r][0];
-      gb2_1 += dr[r][1];
-      gb2_2 += dr[r][2];
-      const float dh = (dr[r][0] * W2_0 + dr[r][1] * W2_1) + dr[r][2] * W2_2;
-      dz1[r] = z1[r] > 0.f ? dh : 0.f;
-      gb1 += dz1[r];
-    }
-    // v_mfma_f32_32x32x2_f32, k = sample pair (2c, 2c+1): A[i][k] = bit i of x_{2c+k}
-    // (lane: i = l & 31, k = l >> 5); B[k][n] = dZ1[2c+k][32 t + n] for tile t, built
-    // from the lane-major dz1 registers by one permlane32 swap.
-    floatx16 acc0 = {}, acc1 = {};
-    const bool hiw = j >= 32;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const uint32_t xsel = hiw ? xb[2 * c + 1] : xb[2 * c];
-      const float av = ((xsel >> (j & 31)) & 1u) ? 1.f : 0.f;
-      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(dz1[2 * c]),
-                                                       __float_as_uint(dz1[2 * c + 1]), false, false);
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av, __uint_as_float(sw[0]), acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av, __uint_as_float(sw[1]), acc1, 0, 0, 0);
-    }
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const int row = (k & 3) + 8 * (k >> 2) + 4 * (j >> 5);
-      if (row < nfsp::OBS) {
-        sm.gW1[w][row * nn::H + (j & 31)] = acc0[k];
-        sm.gW1[w][row * nn::H + 32 + (j & 31)] = acc1[k];
-      }
-    }
-    sm.gW2[w][3 * j + 0] = g2_0;
-    sm.gW2[w][3 * j + 1] = g2_1;
-    sm.gW2[w][3 * j + 2] = g2_2;
-    sm.gb1[w][j] = gb1;
-    if (j == 0) {
-      sm.gb2[w][0] = gb2_0;
-      sm.gb2[w][1] = gb2_1;
-      sm.gb2[w][2] = gb2_2;
-    }
-    CHAIN_STAMP(5);
-    __syncthreads();
-    CHAIN_STAMP(6);
-    // ---- SGD update (fixed reduction order over the 4 wave partials)
-    {
-      float g[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int i = tid + 256 * k;
-        g[k] = 0.f;
-        if (i < nfsp::OBS * nn::H) g[k] = ((sm.gW1[0][i] + sm.gW1[1][i]) + sm.gW1[2][i]) + sm.gW1[3][i];
-      }
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int i = tid + 256 * k;
-        if (i < nfsp::OBS * nn::H) sm.W1[i] = sm.W1[i] - lr * g[k];
-      }
-      float g0 = ((sm.gW2[0][3 * j] + sm.gW2[1][3 * j]) + sm.gW2[2][3 * j]) + sm.gW2[3][3 * j];
-      float g1 = ((sm.gW2[0][3 * j + 1] + sm.gW2[1][3 * j + 1]) + sm.gW2[2][3 * j + 1]) +
-                 sm.gW2[3][3 * j + 1];
-      float g2 = ((sm.gW2[0][3 * j + 2] + sm.gW2[1][3 * j + 2]) + sm.gW2[2][3 * j + 2]) +
-                 sm.gW2[3][3 * j + 2];
-      const float gb = ((sm.gb1[0][j] + sm.gb1[1][j]) + sm.gb1[2][j]) + sm.gb1[3][j];
-      W2_0 = W2_0 - lr * g0;
-      W2_1 = W2_1 - lr * g1;
-      W2_2 = W2_2 - lr * g2;
-      b1 = b1 - lr * gb;
-      g0 = ((sm.gb2[0][0] + sm.gb2[1][0]) + sm.gb2[2][0]) + sm.gb2[3][0];
-      g1 = ((sm.gb2[0][1] + sm.gb2[1][1]) + sm.gb2[2][1]) + sm.gb2[3][1];
-      g2 = ((sm.gb2[0][2] + sm.gb2[1][2]) + sm.gb2[2][2]) + sm.gb2[3][2];
-      b2_0 = b2_0 - lr * g0;
-      b2_1 = b2_1 - lr * g1;
-      b2_2 = b2_2 - lr * g2;
-    }
-    CHAIN_STAMP(7);
-    __syncthreads();
-    CHAIN_STAMP(8);
-    u = nu;
-    e = ne;
-    s = ns;
-  }
-#ifdef NFSP_CHAIN_STAMPS
-  if (C.stamps && j == 0)
-    for (int k = 0; k < 10; ++k) C.stamps[(blockIdx.x * 4 + w) * 10 + k] = st_acc[k];
-#endif
-  // write back (every wave holds identical copies of the small parameters)
-  float* dsts[2] = {gw, C.sync_to[blockIdx.x]};
-  for (int k = 0; k < 2; ++k) {
-    float* dst = dsts[k];
-    if (!dst) continue;
-    for (int i = tid; i < nfsp::OBS * nn::H; i += 256) dst[i] = sm.W1[i];
-    if (w == 0) {
-      dst[nn::OB1 + j] = b1;
-      dst[nn::OW2 + 3 * j + 0] = W2_0;
-      dst[nn::OW2 + 3 * j + 1] = W2_1;
-      dst[nn::OW2 + 3 * j + 2] = W2_2;
-      if (j == 0) {
-        dst[nn::OB2 + 0] = b2_0;
-        dst[nn::OB2 + 1] = b2_1;
-        dst[nn::OB2 + 2] = b2_2;
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// k_chain2: the SGD chain with the 64 hidden units split over the 4 waves (16 each).
-// Every wave sees all 32 samples of a minibatch, so per wave and step
-//   forward   Z1[32 x 16] = X[32 x 32] . W1[:, slice]    16 x v_mfma_f32_16x16x4_f32
-//   backward  dW1[32 x 16] = X^T . dZ1[32 x 16]           16 x v_mfma_f32_16x16x4_f32
-// and the forward's accumulator layout is directly the backward's B operand (samples
-// ordered s(mt, g, r) = 16 mt + 4 g + r, inputs i(Mt, g, r) = 16 Mt + 4 g + r, g = lane >> 4).
-// W1, W2 and b1 of the slice stay in registers and are updated by their own wave; the
-// only cross-wave exchange is the layer-2 output (one barrier per step).  Lane (g, c):
-// hidden 16 w + c; wr[kk] = W1[i(kk >> 2, g, kk & 3)][16 w + c].
-// ---------------------------------------------------------------------------
-typedef float floatx4 __attribute__((ext_vector_type(4)));
-
-struct Chain2Smem {
-  float po[2][4][32][4];     // per-wave partial layer-2 outputs, double-buffered by step parity
-  uint32_t xm[4][32];        // wave-private: the minibatch's 32 observation masks
-  float4 dm[4][32];          // wave-private: dL/dz2 of the 32 samples
-};
 
 __device__ inline float dpp_any(float x, int ctrl) {
   switch (ctrl) {
@@ -717,286 +399,38 @@ __device__ inline float sum_x16(float x) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
-template <int RELU>
-__global__ void __launch_bounds__(256) k_chain2(ChainArgs C) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  Chain2Smem& sm = *reinterpret_cast<Chain2Smem*>(smem_raw);
-  const int a = C.agents[blockIdx.x];
-  const int tid = threadIdx.x;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int l = tid & 63;
-  const int g = l >> 4, c = l & 15;
-  const int hid = 16 * w + c;
-  float* gw = C.w[blockIdx.x];
-  float wr[8];
-#pragma unroll
-  for (int kk = 0; kk < 8; ++kk) {
-    const int i = 16 * (kk >> 2) + 4 * g + (kk & 3);
-    wr[kk] = i < nfsp::OBS ? gw[nn::OW1 + i * nn::H + hid] : 0.f;
-  }
-  float b1 = gw[nn::OB1 + hid];
-  float W2_0 = gw[nn::OW2 + 3 * hid + 0], W2_1 = gw[nn::OW2 + 3 * hid + 1], W2_2 = gw[nn::OW2 + 3 * hid + 2];
-  float b2_0 = gw[nn::OB2 + 0], b2_1 = gw[nn::OB2 + 1], b2_2 = gw[nn::OB2 + 2];
-  const int nmb = C.B / CHAIN_MB;
-  const float inv3m = 1.0f / (float)(3 * CHAIN_MB);
-  const float invm = 1.0f / (float)CHAIN_MB;
-  const int64_t slot0 = (int64_t)a * C.umax;
-  const int64_t u1 = C.u1[blockIdx.x];
-  int64_t u = next_active(C, slot0, C.u0[blockIdx.x], u1);
-  int e = 0, s = 0, buf = 0;
-  uint4 pf = make_uint4(0, 0, 0, 0);          // row of sample (l & 31), one step ahead
-  auto issue = [&](int64_t uu, int ee, int ss) {
-    const uint4* rows = reinterpret_cast<const uint4*>(C.fit + ((slot0 + uu) * C.E + ee) * C.B +
-                                                       ss * CHAIN_MB);
-    pf = rows[l & 31];
-  };
-  if (u < u1) issue(u, e, s);
-  float lr = 0.f;
-#ifdef NFSP_CHAIN_STAMPS
-  unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_last = 0;
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
-#endif
-  while (u < u1) {
-    const uint32_t myx = pf.x;
-    const float tt0 = __uint_as_float(pf.y), tt1 = __uint_as_float(pf.z), tt2 = __uint_as_float(pf.w);
-    if (l < 32) sm.xm[w][l] = myx;
-    if (e == 0 && s == 0)
-      lr = RELU ? (float)(C.lr0 / (1.0 + 0.003 * sqrt((double)(C.it0[blockIdx.x] + 2 * u)))) : C.lr_fixed;
-    int64_t nu = u;
-    int ne = e, ns = s + 1;
-    if (ns == nmb) {
-      ns = 0;
-      if (++ne == C.E) {
-        ne = 0;
-        nu = next_active(C, slot0, u + 1, u1);
-      }
-    }
-    if (nu < u1) issue(nu, ne, ns);
-    const uint32_t xa0 = sm.xm[w][c], xa1 = sm.xm[w][16 + c];
-    uint32_t xs[8];
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) xs[kk] = sm.xm[w][16 * (kk >> 2) + 4 * g + (kk & 3)];
-    CHAIN_STAMP(0);
-    // ---- forward layer 1 on the matrix cores
-    floatx4 z0 = {}, z1 = {};
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) {
-      const int i = 16 * (kk >> 2) + 4 * g + (kk & 3);
-      const float a0 = ((xa0 >> i) & 1u) ? 1.f : 0.f;
-      const float a1 = ((xa1 >> i) & 1u) ? 1.f : 0.f;
-      z0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, wr[kk], z0, 0, 0, 0);
-      z1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, wr[kk], z1, 0, 0, 0);
-    }
-    float zz[8];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      zz[r] = z0[r] + b1;          // sample 4g + r
-      zz[4 + r] = z1[r] + b1;      // sample 16 + 4g + r
-    }
-    CHAIN_STAMP(1);
-    // ---- layer 2, partial over this wave's 16 hidden units: sum over the row's 16 lanes
-    float v[24];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const float h = zz[q] > 0.f ? zz[q] : 0.f;
-      v[3 * q + 0] = h * W2_0;
-      v[3 * q + 1] = h * W2_1;
-      v[3 * q + 2] = h * W2_2;
-    }
-    float hs[12];
-    const bool up = c & 8;
-#pragma unroll
-    for (int i = 0; i < 12; ++i) {      // halve with lane ^ 8, then full sums inside 8 lanes
-      const float keep = up ? v[i + 12] : v[i];
-      const float send = up ? v[i] : v[i + 12];
-      float x = keep + dpp_f(send, 0x128);
-      x = x + dpp_f(x, 0xB1);
-      x = x + dpp_f(x, 0x4E);
-      hs[i] = x + dpp_f(x, 0x141);
-    }
-    if (c == 0 || c == 8) {             // lane c = 0: samples 4g + r; c = 8: 16 + 4g + r
-      const int sb = (c ? 16 : 0) + 4 * g;
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        *reinterpret_cast<float4*>(&sm.po[buf][w][sb + r][0]) =
-            make_float4(hs[3 * r + 0], hs[3 * r + 1], hs[3 * r + 2], 0.f);
-    }
-    CHAIN_STAMP(2);
-    __syncthreads();
-    CHAIN_STAMP(3);
-    // ---- output + loss of sample (l & 31), every wave redundantly (identical results)
-    float d0, d1, d2;
-    {
-      const int sm_i = l & 31;
-      const float4 p0 = *reinterpret_cast<const float4*>(&sm.po[buf][0][sm_i][0]);
-      const float4 p1 = *reinterpret_cast<const float4*>(&sm.po[buf][1][sm_i][0]);
-      const float4 p2 = *reinterpret_cast<const float4*>(&sm.po[buf][2][sm_i][0]);
-      const float4 p3 = *reinterpret_cast<const float4*>(&sm.po[buf][3][sm_i][0]);
-      const float o0 = (((p0.x + p1.x) + p2.x) + p3.x) + b2_0;
-      const float o1 = (((p0.y + p1.y) + p2.y) + p3.y) + b2_1;
-      const float o2 = (((p0.z + p1.z) + p2.z) + p3.z) + b2_2;
-      if (RELU) {
-        const float oz[3] = {o0, o1, o2}, tt[3] = {tt0, tt1, tt2};
-        float dd[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          const float y = oz[k] > 0.f ? oz[k] : 0.f;
-          const float ee = tt[k] - y;
-          const float gg = fabsf(ee) > 1.0f ? (ee > 0.f ? 1.f : (ee < 0.f ? -1.f : 0.f)) : ee;
-          dd[k] = oz[k] > 0.f ? (-gg * inv3m) : 0.f;
-        }
-        d0 = dd[0]; d1 = dd[1]; d2 = dd[2];
-      } else {
-        const float mx = fmaxf(fmaxf(o0, o1), o2);
-        const float e0 = expf(o0 - mx), e1 = expf(o1 - mx), e2 = expf(o2 - mx);
-        const float ssum = (e0 + e1) + e2;
-        const float y[3] = {e0 / ssum, e1 / ssum, e2 / ssum};
-        const float S = (y[0] + y[1]) + y[2];
-        const float eps = 1e-7f, hi = 1.0f - 1e-7f;
-        const float tt[3] = {tt0, tt1, tt2};
-        float dp[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          const float p = y[k] / S;
-          const float pc = fminf(fmaxf(p, eps), hi);
-          const float msk = (p >= eps && p <= hi) ? 1.f : 0.f;
-          dp[k] = (-tt[k] / pc) * msk * invm;
-        }
-        const float dpy = (dp[0] * y[0] + dp[1] * y[1]) + dp[2] * y[2];
-        float dy[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) dy[k] = dp[k] / S - dpy / (S * S);
-        const float dyy = (dy[0] * y[0] + dy[1] * y[1]) + dy[2] * y[2];
-        d0 = y[0] * (dy[0] - dyy);
-        d1 = y[1] * (dy[1] - dyy);
-        d2 = y[2] * (dy[2] - dyy);
-      }
-    }
-    if (l < 32) sm.dm[w][l] = make_float4(d0, d1, d2, 0.f);
-    // gb2 = sum over the 32 samples (lanes 32..63 mirror 0..31)
-    float gb2[3] = {d0, d1, d2};
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      float x = gb2[k];
-      x = x + dpp_any(x, 0x128);
-      x = x + dpp_any(x, 0x124);
-      x = x + dpp_any(x, 0x122);
-      x = x + dpp_any(x, 0x121);
-      gb2[k] = sum_x16(x);
-    }
-    CHAIN_STAMP(4);
-    // ---- backward: dZ1 in the forward's accumulator layout, layer-2 / bias gradients
-    float dz[8];
-    float g2_0 = 0.f, g2_1 = 0.f, g2_2 = 0.f, gb1 = 0.f;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const float4 dd = sm.dm[w][16 * (q >> 2) + 4 * g + (q & 3)];
-      const float h = zz[q] > 0.f ? zz[q] : 0.f;
-      g2_0 += h * dd.x;
-      g2_1 += h * dd.y;
-      g2_2 += h * dd.z;
-      const float dh = (dd.x * W2_0 + dd.y * W2_1) + dd.z * W2_2;
-      dz[q] = zz[q] > 0.f ? dh : 0.f;
-      gb1 += dz[q];
-    }
-    g2_0 = sum_x16(sum_x32(g2_0));
-    g2_1 = sum_x16(sum_x32(g2_1));
-    g2_2 = sum_x16(sum_x32(g2_2));
-    gb1 = sum_x16(sum_x32(gb1));
-    CHAIN_STAMP(5);
-    // dW1[i][hid] = sum_s x_s[i] dZ1[s][hid]: k-step kk = samples s(kk >> 2, g, kk & 3)
-    floatx4 gA = {}, gB = {};
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) {
-      const float a0 = ((xs[kk] >> c) & 1u) ? 1.f : 0.f;          // input c
-      const float a1 = ((xs[kk] >> (16 + c)) & 1u) ? 1.f : 0.f;   // input 16 + c
-      gA = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, dz[kk], gA, 0, 0, 0);
-      gB = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, dz[kk], gB, 0, 0, 0);
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      wr[r] = wr[r] - lr * gA[r];          // input 4g + r
-      wr[4 + r] = wr[4 + r] - lr * gB[r];  // input 16 + 4g + r
-    }
-    W2_0 = W2_0 - lr * g2_0;
-    W2_1 = W2_1 - lr * g2_1;
-    W2_2 = W2_2 - lr * g2_2;
-    b1 = b1 - lr * gb1;
-    b2_0 = b2_0 - lr * gb2[0];
-    b2_1 = b2_1 - lr * gb2[1];
-    b2_2 = b2_2 - lr * gb2[2];
-    CHAIN_STAMP(6);
-    buf ^= 1;
-    u = nu;
-    e = ne;
-    s = ns;
-  }
-#ifdef NFSP_CHAIN_STAMPS
-  if (C.stamps && l == 0)
-    for (int k = 0; k < 10; ++k) C.stamps[(blockIdx.x * 4 + w) * 10 + k] = st_acc[k];
-#endif
-  float* dsts[2] = {gw, C.sync_to[blockIdx.x]};
-  for (int k = 0; k < 2; ++k) {
-    float* dst = dsts[k];
-    if (!dst) continue;
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) {
-      const int i = 16 * (kk >> 2) + 4 * g + (kk & 3);
-      if (i < nfsp::OBS) dst[nn::OW1 + i * nn::H + hid] = wr[kk];
-    }
-    if (g == 0) {
-      dst[nn::OB1 + hid] = b1;
-      dst[nn::OW2 + 3 * hid + 0] = W2_0;
-      dst[nn::OW2 + 3 * hid + 1] = W2_1;
-      dst[nn::OW2 + 3 * hid + 2] = W2_2;
-    }
-    if (w == 0 && l == 0) {
-      dst[nn::OB2 + 0] = b2_0;
-      dst[nn::OB2 + 1] = b2_1;
-      dst[nn::OB2 + 2] = b2_2;
-    }
-  }
-}
-
 // ---------------------------------------------------------------------------
 // k_chain3: the SGD chain on bf16 matrix cores with exact-f32 operands.
 //
 // An f32 value v is split exactly into three bf16 terms v = hi + mid + lo (8 + 8 + 8
 // significand bits, round-to-nearest at each cut), and a Leduc observation is 0/1, so
 // X.W = X.lo + X.mid + X.hi with every product exact and f32 accumulation: the 16 chained
-// v_mfma_f32_16x16x4_f32 of a layer-1 product become 6 v_mfma_f32_16x16x32_bf16 (K = 32
-// covers all 30 inputs).  Per wave (hidden slice 16w..16w+15, lane (g, c) = (l >> 4, l & 15)):
+// v_mfma_f32_16x16x4_f32 of a layer-1 product become 3 v_mfma_f32_16x16x32_bf16 per tile
+// (K = 32 covers all 30 inputs).  Per wave (hidden slice 16w..16w+15, lane (g, c) =
+// (l >> 4, l & 15)):
 //   * layer-1 K slot 8g + j <-> input pi(g, j) = 4g + j (j < 4) or 16 + 4g + j - 4, so the
 //     dW1 accumulator lands in the registers that hold W1 (wr[j] = W1[pi(g, j)][16w + c]);
 //   * forward twice from the same registers: Z1 sample-major (D row = sample, for the
 //     backward and dW1) and Z1^T hidden-major (D row = hidden: layer 2 is then 4 lane-local
 //     FMAs per output plus two permlane swaps instead of a 16-lane reduction);
-//   * dW1 = X^T dZ1 with K = samples: the A operand comes from the bit-transposed masks
-//     (xt) the prep kernels emit, the B operand is dZ1 split the same way;
-//   * operands of step t+1 are formed during step t from rows loaded two steps ahead
-//     (two named buffers, loop unrolled by two: no load result is ever copied);
-//   * one barrier per step (the 4 waves' layer-2 partials), all other exchange is
+//   * dW1 = X^T dZ1 with K = samples (K slot 8g + j <-> sample 16 (j >> 2) + 4g + (j & 3));
+//   * every bit operand comes ready-made from the step record (StepRec: the prep kernels
+//     expand the masks and their bit transpose), loaded three steps ahead into three named
+//     buffers (loop unrolled by three: no load result is ever copied);
+//   * one barrier per step (the 4 waves' layer-2 partials); all other exchange is
 //     wave-private (LDS dm / w2t) or cross-lane (DPP, permlane).
 // ---------------------------------------------------------------------------
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
 
 struct Chain3Smem {
   float po[2][4][32][4];     // per-wave partial layer-2 outputs, double-buffered by step parity
   float dm[4][3][32];        // wave-private: dL/dz2 of the 32 samples, by output
   float4 w2t[4][16];         // wave-private: (W2[h][0..2], b1[h]) of the slice, for Z1^T
 };
-
-// 8 bf16 0/1 values of the K slots 8g..8g+7 from a 32-bit mask: bits 4g..4g+3, 16+4g..+3
-__device__ inline bf16x8 bits8(uint32_t x, int g) {
-  const uint32_t n0 = (x >> (4 * g)) & 0xFu, n1 = (x >> (16 + 4 * g)) & 0xFu;
-  u32x4v r;
-  r[0] = (n0 & 1u) * 0x3F80u + ((n0 >> 1) & 1u) * 0x3F800000u;
-  r[1] = ((n0 >> 2) & 1u) * 0x3F80u + ((n0 >> 3) & 1u) * 0x3F800000u;
-  r[2] = (n1 & 1u) * 0x3F80u + ((n1 >> 1) & 1u) * 0x3F800000u;
-  r[3] = ((n1 >> 2) & 1u) * 0x3F80u + ((n1 >> 3) & 1u) * 0x3F800000u;
-  return __builtin_bit_cast(bf16x8, r);
-}
+// Reserve (nearly) all of a CU's LDS for a chain workgroup: a chain then has its CU to
+// itself -- no prep / target kernel's waves share its SIMDs.
+constexpr int CHAIN_LDS = 150 * 1024;
+static_assert(sizeof(Chain3Smem) <= CHAIN_LDS, "chain LDS");
 
 // exact three-term bf16 split of 8 f32 values
 __device__ inline void split3(const float (&v)[8], bf16x8& hi, bf16x8& mid, bf16x8& lo) {
@@ -1026,16 +460,10 @@ __device__ inline floatx4 mfma3t(bf16x8 ahi, bf16x8 amid, bf16x8 alo, bf16x8 b) 
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, b, z, 0, 0, 0);
 }
 
-struct C3Buf {               // one step's loads (lane-specific)
-  uint4 ra, rb;              // fit rows c and 16 + c: (x, t0, t1, t2)
-  uint32_t xa, xb;           // xt words c and 16 + c
-  float lr;
-};
-struct C3Ops {               // one step's operands, formed a step ahead
+struct C3Buf {               // one step's operands (lane-specific), loaded from its StepRec
   bf16x8 fa0, fa1;           // X bits of samples c / 16 + c (Z1 A operand, Z1^T B operand)
   bf16x8 ba0, ba1;           // X^T bits of inputs c / 16 + c over the samples (dW1 A operand)
-  float t0, t1, t2;          // fit targets of this lane's loss sample 16 (g >> 1) + c
-  float lr;
+  float4 tg;                 // targets of this lane's loss sample 16 (g >> 1) + c, and lr
 };
 
 template <int RELU>
@@ -1077,31 +505,16 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
   }
   const int T1 = (int)(u1 * spu);
   int t = (int)(u0 * spu);
-  const uint4* fitb = reinterpret_cast<const uint4*>(C.fit + slot0 * C.E * C.B);
-  const uint32_t* xtb = C.xt + slot0 * C.E * C.B;
-  const float* lrb = RELU ? C.lr_tab + slot0 : nullptr;
-  // loader position (the step whose rows the next load_next fetches) and its update
-  int lpos = t, lu = (int)u0, lk = 0;
+  const StepRec* recb = C.rec + slot0 * spu;
+  int lpos = t;                                // the step whose record load_next fetches
   auto load_next = [&](C3Buf& b) {
-    const int p = lpos < T1 ? lpos : T1 - 1;
-    b.ra = fitb[32 * p + c];
-    b.rb = fitb[32 * p + 16 + c];
-    b.xa = xtb[32 * p + c];
-    b.xb = xtb[32 * p + 16 + c];
-    b.lr = RELU ? lrb[lu < u1 ? lu : u1 - 1] : C.lr_fixed;
+    const StepRec& R = recb[lpos < T1 ? lpos : T1 - 1];
+    b.fa0 = __builtin_bit_cast(bf16x8, R.fa[g][c]);
+    b.fa1 = __builtin_bit_cast(bf16x8, R.fa[g][16 + c]);
+    b.ba0 = __builtin_bit_cast(bf16x8, R.ba[g][c]);
+    b.ba1 = __builtin_bit_cast(bf16x8, R.ba[g][16 + c]);
+    b.tg = R.tg[sl];
     ++lpos;
-    if (++lk == spu) { lk = 0; ++lu; }
-  };
-  auto make_ops = [&](C3Ops& o, const C3Buf& b) {
-    o.fa0 = bits8(b.ra.x, g);
-    o.fa1 = bits8(b.rb.x, g);
-    o.ba0 = bits8(b.xa, g);
-    o.ba1 = bits8(b.xb, g);
-    const uint4 tr = (g >> 1) ? b.rb : b.ra;
-    o.t0 = __uint_as_float(tr.y);
-    o.t1 = __uint_as_float(tr.z);
-    o.t2 = __uint_as_float(tr.w);
-    o.lr = b.lr;
   };
   auto publish = [&]() {   // this wave's (W2, b1) rows for its own Z1^T layer 2
     if (g == 0) sm.w2t[w][c] = make_float4(W2_0, W2_1, W2_2, b1);
@@ -1110,8 +523,7 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
   unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_last = 0;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
 #endif
-  auto step = [&](const C3Ops& o, C3Buf& mine, C3Ops& nxt, const C3Buf& other) {
-    load_next(mine);                               // rows of step t + 2
+  auto step = [&](C3Buf& o) {
     // ---- layer 1, both orientations
     bf16x8 whi, wmid, wlo;
     split3(wr, whi, wmid, wlo);
@@ -1162,7 +574,7 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
       const float o0 = (((a0.x + a1.x) + a2.x) + a3.x) + b2_0;
       const float o1 = (((a0.y + a1.y) + a2.y) + a3.y) + b2_1;
       const float o2 = (((a0.z + a1.z) + a2.z) + a3.z) + b2_2;
-      const float tt[3] = {o.t0, o.t1, o.t2};
+      const float tt[3] = {o.tg.x, o.tg.y, o.tg.z};
       if (RELU) {          // Huber on ReLU outputs, mean over 3 x batch
         const float oz[3] = {o0, o1, o2};
         float dd[3];
@@ -1243,8 +655,7 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
     }
     bf16x8 dhi, dmid, dlo;
     split3(dz, dhi, dmid, dlo);
-    // dW1[16 it + 4g + r][16w + c] = sum over the 32 samples (K slot 8g + j <-> sample
-    // 16 (j >> 2) + 4g + (j & 3), the order of dz)
+    // dW1[16 it + 4g + r][16w + c] = sum over the 32 samples in dz's K order
     const floatx4 gA = mfma3(o.ba0, dhi, dmid, dlo);
     const floatx4 gB = mfma3(o.ba1, dhi, dmid, dlo);
     g2_0 = sum_x16(sum_x32(g2_0));
@@ -1252,7 +663,7 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
     g2_2 = sum_x16(sum_x32(g2_2));
     gb1 = sum_x16(sum_x32(gb1));
     CHAIN_STAMP(4);
-    const float lr = o.lr;
+    const float lr = o.tg.w;
     W2_0 = W2_0 - lr * g2_0;
     W2_1 = W2_1 - lr * g2_1;
     W2_2 = W2_2 - lr * g2_2;
@@ -1261,25 +672,26 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
     b2_1 = b2_1 - lr * gb2[1];
     b2_2 = b2_2 - lr * gb2[2];
     publish();
-    make_ops(nxt, other);                          // operands of step t + 1
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       wr[r] = wr[r] - lr * gA[r];
       wr[4 + r] = wr[4 + r] - lr * gB[r];
     }
+    load_next(o);                                  // step t + 3 into the consumed buffer
     CHAIN_STAMP(5);
   };
   if (t < T1) {
-    C3Buf bA, bB;
-    C3Ops oA, oB;
-    load_next(bA);
-    load_next(bB);
-    make_ops(oA, bA);
+    C3Buf b0, b1r, b2r;
+    load_next(b0);
+    load_next(b1r);
+    load_next(b2r);
     publish();
     for (;;) {
-      step(oA, bA, oB, bB);
+      step(b0);
       if (++t >= T1) break;
-      step(oB, bB, oA, bA);
+      step(b1r);
+      if (++t >= T1) break;
+      step(b2r);
       if (++t >= T1) break;
     }
   }
@@ -1356,7 +768,7 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
   NFSP_HIP(hipStreamSynchronize(s));
   KTimer kt(e, KT_LEARNER);
   e->learn_tag++;
-  PrepArgs P;
+  PrepArgs P{};
   P.M = e->M;
   P.LB = e->LB;
   P.st = e->st;
@@ -1367,6 +779,7 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
   P.k0 = (uint32_t)cfg.seed;
   P.k1 = (uint32_t)(cfg.seed >> 32);
   P.tag = e->learn_tag;
+  P.lr_ar = cfg.lr_ar;
   int64_t maxU = 0, maxUbr = 0, maxSL = 0;
   for (int a = 0; a < 2; ++a) {
     AgentPlan& pl = P.A[a];
@@ -1407,10 +820,10 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
   }
   static bool attr = false;
   if (!attr) {
-    NFSP_HIP(hipFuncSetAttribute((const void*)k_chain2<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)sizeof(Chain2Smem)));
-    NFSP_HIP(hipFuncSetAttribute((const void*)k_chain2<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 (int)sizeof(Chain2Smem)));
+    NFSP_HIP(hipFuncSetAttribute((const void*)k_chain3<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 CHAIN_LDS));
+    NFSP_HIP(hipFuncSetAttribute((const void*)k_chain3<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 CHAIN_LDS));
     attr = true;
   }
   hipEvent_t fork = take_event(e);
@@ -1419,14 +832,11 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
   if (maxU > 0) {
     NFSP_HIP(hipStreamWaitEvent(e->s_ar, fork, 0));
     ChainArgs C{};
-    C.fit = e->LB.ar_fit;
-    C.xt = e->LB.ar_xt;
+    C.rec = e->LB.ar_rec;
     C.active = e->LB.ar_active;
     C.umax = e->LB.umax;
     C.B = cfg.batch;
     C.E = cfg.epochs;
-    C.relu = 0;
-    C.lr_fixed = cfg.lr_ar;
     for (int a = 0; a < 2; ++a) {
       C.agents[a] = a;
       C.w[a] = e->w + (a * 3 + 0) * nn::NP;
@@ -1435,7 +845,7 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
       C.u1[a] = P.A[a].U;
     }
     KTimer kc(e, KT_CHAIN_AR, e->s_ar);
-    k_chain3<0><<<2, 256, sizeof(Chain3Smem), e->s_ar>>>(C);
+    k_chain3<0><<<2, 256, CHAIN_LDS, e->s_ar>>>(C);
     NFSP_LAUNCHED("k_chain(AR)");
   }
   // ---- BR: per agent, segments between target syncs, each = targets + chain
@@ -1473,24 +883,19 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
       }
       NFSP_LAUNCHED("k_br_targets");
       ChainArgs C{};
-      C.fit = e->LB.br_fit;
-      C.xt = e->LB.br_xt;
-      C.lr_tab = e->LB.br_lr;
+      C.rec = e->LB.br_rec;
       C.active = nullptr;
       C.umax = e->LB.umax;
       C.B = cfg.batch;
       C.E = cfg.epochs;
-      C.relu = 1;
-      C.lr0 = cfg.lr_br;
       C.agents[0] = a;
       C.w[0] = wbr;
       C.sync_to[0] = sync ? wtg : nullptr;
       C.u0[0] = u;
       C.u1[0] = v;
-      C.it0[0] = it0;
       {
         KTimer kc(e, KT_CHAIN_BR, sa);
-        k_chain3<1><<<1, 256, sizeof(Chain3Smem), sa>>>(C);
+        k_chain3<1><<<1, 256, CHAIN_LDS, sa>>>(C);
       }
       NFSP_LAUNCHED("k_chain(BR)");
       u = v;

@@ -97,7 +97,7 @@ class SelfPlayEngine:
         return s.to_dict()
 
     KERNELS = ("k_rollout", "k_scan", "k_commit", "learner", "learner_prep", "k_br_targets",
-               "k_chain2_br", "k_chain2_ar")
+               "k_chain3_br", "k_chain3_ar")
 
     def set_timing(self, on=True):
         native.check(self.L.nfsp_engine_set_timing(self.h, int(bool(on))), "set_timing")
