@@ -19,6 +19,7 @@
 // BR chains are cut into segments at target-sync points; the two agents' BR chains and
 // the AR chains run on separate streams.
 #include <math.h>
+#include <stdlib.h>
 
 #include "engine_internal.h"
 
@@ -415,18 +416,27 @@ __device__ inline float sum_x16(float x) {
 //     FMAs per output plus two permlane swaps instead of a 16-lane reduction);
 //   * dW1 = X^T dZ1 with K = samples (K slot 8g + j <-> sample 16 (j >> 2) + 4g + (j & 3));
 //   * every bit operand comes ready-made from the step record (StepRec: the prep kernels
-//     expand the masks and their bit transpose), loaded three steps ahead into three named
-//     buffers (loop unrolled by three: no load result is ever copied);
+//     expand the masks and their bit transpose), loaded three steps ahead into four named
+//     buffers (loop unrolled by four: no load result is ever copied);
 //   * one barrier per step (the 4 waves' layer-2 partials); all other exchange is
 //     wave-private (LDS dm / w2t) or cross-lane (DPP, permlane).
 // ---------------------------------------------------------------------------
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
+#ifdef NFSP_CHAIN_STAMPS
+// diagnostic build: [AR blk 0, AR blk 1, BR, -][wave][phase 0-5, -, -, kernel cycles, steps]
+__device__ unsigned long long g_chain_stamps[4][4][10];
+#endif
+
 struct Chain3Smem {
   float po[2][4][32][4];     // per-wave partial layer-2 outputs, double-buffered by step parity
   float dm[4][3][32];        // wave-private: dL/dz2 of the 32 samples, by output
   float4 w2t[4][16];         // wave-private: (W2[h][0..2], b1[h]) of the slice, for Z1^T
+  StepRec ring[4];           // step records t .. t + 2 (slot t & 3), a quarter per wave
 };
+constexpr int REC_CHUNKS = (int)(sizeof(StepRec) / 16);    // 288 x 16 B
+constexpr int REC_QUARTER = REC_CHUNKS / 4;                 // 72 per wave
+static_assert(REC_CHUNKS % 4 == 0 && REC_QUARTER > 64 && REC_QUARTER <= 128, "record chunking");
 // Reserve (nearly) all of a CU's LDS for a chain workgroup: a chain then has its CU to
 // itself -- no prep / target kernel's waves share its SIMDs.
 constexpr int CHAIN_LDS = 150 * 1024;
@@ -459,12 +469,6 @@ __device__ inline floatx4 mfma3t(bf16x8 ahi, bf16x8 amid, bf16x8 alo, bf16x8 b) 
   z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(amid, b, z, 0, 0, 0);
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, b, z, 0, 0, 0);
 }
-
-struct C3Buf {               // one step's operands (lane-specific), loaded from its StepRec
-  bf16x8 fa0, fa1;           // X bits of samples c / 16 + c (Z1 A operand, Z1^T B operand)
-  bf16x8 ba0, ba1;           // X^T bits of inputs c / 16 + c over the samples (dW1 A operand)
-  float4 tg;                 // targets of this lane's loss sample 16 (g >> 1) + c, and lr
-};
 
 template <int RELU>
 __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
@@ -505,16 +509,17 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
   }
   const int T1 = (int)(u1 * spu);
   int t = (int)(u0 * spu);
-  const StepRec* recb = C.rec + slot0 * spu;
-  int lpos = t;                                // the step whose record load_next fetches
-  auto load_next = [&](C3Buf& b) {
-    const StepRec& R = recb[lpos < T1 ? lpos : T1 - 1];
-    b.fa0 = __builtin_bit_cast(bf16x8, R.fa[g][c]);
-    b.fa1 = __builtin_bit_cast(bf16x8, R.fa[g][16 + c]);
-    b.ba0 = __builtin_bit_cast(bf16x8, R.ba[g][c]);
-    b.ba1 = __builtin_bit_cast(bf16x8, R.ba[g][16 + c]);
-    b.tg = R.tg[sl];
-    ++lpos;
+  const uint4* recb = reinterpret_cast<const uint4*>(C.rec + slot0 * spu);
+  // this wave's quarter of record p (clamped), into two registers / back into ring slot p & 3
+  auto issue = [&](int p, uint4& va, uint4& vb) {
+    const uint4* src = recb + (size_t)(p < T1 ? p : T1 - 1) * REC_CHUNKS + REC_QUARTER * w;
+    va = src[l];
+    vb = l < REC_QUARTER - 64 ? src[64 + l] : make_uint4(0, 0, 0, 0);
+  };
+  auto stash = [&](int p, const uint4& va, const uint4& vb) {
+    uint4* dst = reinterpret_cast<uint4*>(&sm.ring[p & 3]) + REC_QUARTER * w;
+    dst[l] = va;
+    if (l < REC_QUARTER - 64) dst[64 + l] = vb;
   };
   auto publish = [&]() {   // this wave's (W2, b1) rows for its own Z1^T layer 2
     if (g == 0) sm.w2t[w][c] = make_float4(W2_0, W2_1, W2_2, b1);
@@ -522,8 +527,20 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
 #ifdef NFSP_CHAIN_STAMPS
   unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_last = 0;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
+  const unsigned long long st_t0 = st_last;
 #endif
-  auto step = [&](C3Buf& o) {
+  // Records reach the lanes through an LDS ring: at step t each wave loads its quarter of
+  // record t + 2 and stores it at the end of step t; barrier(t + 1) publishes it.  Every
+  // load is consumed inside its own step (nothing loop-carried in registers), and the 4
+  // waves share one copy of each record.
+  auto step = [&]() {
+    uint4 va, vb;
+    issue(t + 2, va, vb);
+    const StepRec& R = sm.ring[t & 3];
+    const bf16x8 fa0 = __builtin_bit_cast(bf16x8, R.fa[g][c]);
+    const bf16x8 fa1 = __builtin_bit_cast(bf16x8, R.fa[g][16 + c]);
+    const bf16x8 ba0 = __builtin_bit_cast(bf16x8, R.ba[g][c]);
+    const bf16x8 ba1 = __builtin_bit_cast(bf16x8, R.ba[g][16 + c]);
     // ---- layer 1, both orientations
     bf16x8 whi, wmid, wlo;
     split3(wr, whi, wmid, wlo);
@@ -533,10 +550,10 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
       const float4 q = sm.w2t[w][4 * g + r];
       W2h[r][0] = q.x; W2h[r][1] = q.y; W2h[r][2] = q.z; b1h[r] = q.w;
     }
-    const floatx4 zh0 = mfma3t(whi, wmid, wlo, o.fa0);   // Z1^T: hidden 16w+4g+r, sample c
-    const floatx4 zh1 = mfma3t(whi, wmid, wlo, o.fa1);   //                      sample 16+c
-    const floatx4 zs0 = mfma3(o.fa0, whi, wmid, wlo);    // Z1: sample 4g+r, hidden 16w+c
-    const floatx4 zs1 = mfma3(o.fa1, whi, wmid, wlo);    //     sample 16+4g+r
+    const floatx4 zh0 = mfma3t(whi, wmid, wlo, fa0);     // Z1^T: hidden 16w+4g+r, sample c
+    const floatx4 zh1 = mfma3t(whi, wmid, wlo, fa1);     //                      sample 16+c
+    const floatx4 zs0 = mfma3(fa0, whi, wmid, wlo);      // Z1: sample 4g+r, hidden 16w+c
+    const floatx4 zs1 = mfma3(fa1, whi, wmid, wlo);      //     sample 16+4g+r
     CHAIN_STAMP(0);
     // ---- layer 2 partial over the slice, from Z1^T
     float p0[3], p1[3];
@@ -565,7 +582,7 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
     __syncthreads();
     CHAIN_STAMP(2);
     // ---- output + loss of sample sl (every wave redundantly, identical results)
-    float d0, d1, d2;
+    float d0, d1, d2, lr_step;
     {
       const float4 a0 = *reinterpret_cast<const float4*>(&sm.po[buf][0][sl][0]);
       const float4 a1 = *reinterpret_cast<const float4*>(&sm.po[buf][1][sl][0]);
@@ -574,7 +591,9 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
       const float o0 = (((a0.x + a1.x) + a2.x) + a3.x) + b2_0;
       const float o1 = (((a0.y + a1.y) + a2.y) + a3.y) + b2_1;
       const float o2 = (((a0.z + a1.z) + a2.z) + a3.z) + b2_2;
-      const float tt[3] = {o.tg.x, o.tg.y, o.tg.z};
+      const float4 tg = R.tg[sl];
+      lr_step = tg.w;
+      const float tt[3] = {tg.x, tg.y, tg.z};
       if (RELU) {          // Huber on ReLU outputs, mean over 3 x batch
         const float oz[3] = {o0, o1, o2};
         float dd[3];
@@ -656,14 +675,14 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
     bf16x8 dhi, dmid, dlo;
     split3(dz, dhi, dmid, dlo);
     // dW1[16 it + 4g + r][16w + c] = sum over the 32 samples in dz's K order
-    const floatx4 gA = mfma3(o.ba0, dhi, dmid, dlo);
-    const floatx4 gB = mfma3(o.ba1, dhi, dmid, dlo);
+    const floatx4 gA = mfma3(ba0, dhi, dmid, dlo);
+    const floatx4 gB = mfma3(ba1, dhi, dmid, dlo);
     g2_0 = sum_x16(sum_x32(g2_0));
     g2_1 = sum_x16(sum_x32(g2_1));
     g2_2 = sum_x16(sum_x32(g2_2));
     gb1 = sum_x16(sum_x32(gb1));
     CHAIN_STAMP(4);
-    const float lr = o.tg.w;
+    const float lr = lr_step;
     W2_0 = W2_0 - lr * g2_0;
     W2_1 = W2_1 - lr * g2_1;
     W2_2 = W2_2 - lr * g2_2;
@@ -677,27 +696,36 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
       wr[r] = wr[r] - lr * gA[r];
       wr[4 + r] = wr[4 + r] - lr * gB[r];
     }
-    load_next(o);                                  // step t + 3 into the consumed buffer
+    stash(t + 2, va, vb);
     CHAIN_STAMP(5);
   };
   if (t < T1) {
-    C3Buf b0, b1r, b2r;
-    load_next(b0);
-    load_next(b1r);
-    load_next(b2r);
-    publish();
-    for (;;) {
-      step(b0);
-      if (++t >= T1) break;
-      step(b1r);
-      if (++t >= T1) break;
-      step(b2r);
-      if (++t >= T1) break;
+    {
+      uint4 va, vb;
+      issue(t, va, vb);
+      stash(t, va, vb);
+      issue(t + 1, va, vb);
+      stash(t + 1, va, vb);
     }
+    publish();
+    __syncthreads();
+    // drain the prologue's loads: the loop header then merges no pending load into the
+    // registers the loop reuses (else every step waits on its fresh record load)
+    __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0) (gfx9 encoding: expcnt 7, lgkmcnt 15)
+    for (; t < T1; ++t) step();
   }
 #ifdef NFSP_CHAIN_STAMPS
-  if (C.stamps && l == 0)
-    for (int k = 0; k < 10; ++k) C.stamps[(blockIdx.x * 4 + w) * 10 + k] = st_acc[k];
+  if (l == 0) {
+    unsigned long long t_end;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_end)::"memory");
+    st_acc[8] = t_end - st_t0;
+    st_acc[9] = (unsigned long long)(T1 - (int)(u0 * spu));
+    if (C.stamps) {
+      for (int k = 0; k < 10; ++k) C.stamps[(blockIdx.x * 4 + w) * 10 + k] = st_acc[k];
+    } else {       // engine build: accumulate per (net, block, wave) for nfsp_debug_chain_stamps
+      for (int k = 0; k < 10; ++k) atomicAdd(&g_chain_stamps[RELU * 2 + blockIdx.x][w][k], st_acc[k]);
+    }
+  }
 #endif
   float* dsts[2] = {gw, C.sync_to[blockIdx.x]};
   for (int k = 0; k < 2; ++k) {
@@ -755,6 +783,15 @@ __global__ void k_finalize(FinalArgs F) {
 }
 
 }  // namespace
+
+#ifdef NFSP_CHAIN_STAMPS
+// diagnostic build only: the accumulated chain phase cycles ([4][4][10] u64), then reset
+extern "C" int nfsp_debug_chain_stamps(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_chain_stamps), sizeof(g_chain_stamps)) != hipSuccess) return -1;
+  static const unsigned long long zero[4][4][10] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_chain_stamps), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" int nfsp_engine_update(nfsp_engine* e) {
   NFSP_REQUIRE(e, "null argument");
@@ -848,6 +885,13 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
     k_chain3<0><<<2, 256, CHAIN_LDS, e->s_ar>>>(C);
     NFSP_LAUNCHED("k_chain(AR)");
   }
+  // diagnostic (NFSP_LEARNER_SERIAL=1): BR work waits for the AR chains, to time them alone
+  static const bool serial_ar = getenv("NFSP_LEARNER_SERIAL") && atoi(getenv("NFSP_LEARNER_SERIAL"));
+  hipEvent_t ar_done = fork;
+  if (serial_ar) {
+    ar_done = take_event(e);
+    NFSP_HIP(hipEventRecord(ar_done, e->s_ar));
+  }
   // ---- BR: per agent, segments between target syncs, each = targets + chain
   FinalArgs F{};
   F.st = e->st;
@@ -860,7 +904,7 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
     F.n_sl[a] = pl.n_sl;
     F.U_br[a] = pl.U_br;
     hipStream_t sa = e->s_br[a];
-    NFSP_HIP(hipStreamWaitEvent(sa, fork, 0));
+    NFSP_HIP(hipStreamWaitEvent(sa, serial_ar ? ar_done : fork, 0));
     int64_t it = h.iteration[a], tc = h.target_count[a], syncs = h.target_syncs[a];
     double eps = h.epsilon[a];
     const int64_t it0 = it;
@@ -922,6 +966,7 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
     e->pool.push_back(j);      // reusable once the wait is enqueued
   }
   e->pool.push_back(fork);
+  if (ar_done != fork) e->pool.push_back(ar_done);
   k_finalize<<<1, 64, 0, s>>>(F);
   NFSP_LAUNCHED("k_finalize");
   return NFSP_OK;

@@ -3,7 +3,7 @@
 // split of waves 0..3 (s_memtime).  Mode "compare" checks k_chain3 against the previous
 // f32-MFMA chain (tools/chain_ref.hip) from the same start.  Not part of libnfsp.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude -I<pkg>/csrc tools/bench_chain.hip
-//   ./bench_chain <updates> <relu 0|1> [time|compare]
+//   ./bench_chain <updates> <relu 0|1> [time|compare] [blocks 1|2]
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -36,6 +36,7 @@ int main(int argc, char** argv) {
   const int U = argc > 1 ? atoi(argv[1]) : 200;
   const int relu = argc > 2 ? atoi(argv[2]) : 1;
   const bool compare = argc > 3 && !strcmp(argv[3], "compare");
+  const int nblk = argc > 4 ? atoi(argv[4]) : 1;     // concurrent chains (as the AR launch: 2)
   const int B = 128, E = 2, NMB = B / 32;
   std::mt19937 rng(7);
   std::vector<chainref::FitRow> fit((size_t)U * E * B);
@@ -74,16 +75,20 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(dfit, fit.data(), fit.size() * sizeof(chainref::FitRow), hipMemcpyHostToDevice));
   CK(hipMemcpy(drec, rec.data(), rec.size() * sizeof(StepRec), hipMemcpyHostToDevice));
   CK(hipMemcpy(dw, w.data(), w.size() * 4, hipMemcpyHostToDevice));
+  float* dw2;
+  CK(hipMalloc(&dw2, w.size() * 4));
+  CK(hipMemcpy(dw2, w.data(), w.size() * 4, hipMemcpyHostToDevice));
   ChainArgs C{};
   C.w[0] = dw; C.rec = drec; C.umax = U; C.u0[0] = 0; C.u1[0] = U; C.B = B; C.E = E; C.stamps = dst;
+  C.w[1] = dw2; C.u0[1] = 0; C.u1[1] = U;            // second chain: same records, own weights
   chainref::RefArgs R{};
   R.w[0] = dw; R.fit = dfit; R.umax = U; R.u0[0] = 0; R.u1[0] = U; R.B = B; R.E = E;
   R.lr_fixed = 0.1f; R.lr0 = 0.05;
   CK(hipFuncSetAttribute((const void*)k_chain3<0>, hipFuncAttributeMaxDynamicSharedMemorySize, CHAIN_LDS));
   CK(hipFuncSetAttribute((const void*)k_chain3<1>, hipFuncAttributeMaxDynamicSharedMemorySize, CHAIN_LDS));
   auto launch3 = [&]() {
-    if (relu) k_chain3<1><<<1, 256, CHAIN_LDS>>>(C);
-    else k_chain3<0><<<1, 256, CHAIN_LDS>>>(C);
+    if (relu) k_chain3<1><<<nblk, 256, CHAIN_LDS>>>(C);
+    else k_chain3<0><<<nblk, 256, CHAIN_LDS>>>(C);
   };
   if (compare) {
     std::vector<float> out[2];
@@ -121,8 +126,8 @@ int main(int argc, char** argv) {
   std::vector<float> wout(nn::NP);
   CK(hipMemcpy(wout.data(), dw, wout.size() * 4, hipMemcpyDeviceToHost));
   double cs = 0; for (float v : wout) cs += v;
-  printf("k_chain3 checksum=%.9g relu=%d updates=%d sgd_steps=%d  %.3f ms  %.3f us/step  %.2f us/update\n",
-         cs, relu, U, steps, ms, ms * 1e3 / steps, ms * 1e3 / U);
+  printf("k_chain3 blocks=%d checksum=%.9g relu=%d updates=%d sgd_steps=%d  %.3f ms  %.3f us/step  %.2f us/update\n",
+         nblk, cs, relu, U, steps, ms, ms * 1e3 / steps, ms * 1e3 / U);
   std::vector<unsigned long long> st(80);
   CK(hipMemcpy(st.data(), dst, 80 * 8, hipMemcpyDeviceToHost));
   const char* names[6] = {"fwd-mfma", "layer2+po", "barrier", "loss+gb2", "bwd+dW1", "update+load"};
