@@ -91,6 +91,53 @@ def cpu_baseline(seconds: float):
                       f"{dt:.1f} s on one core"}
 
 
+def init_dist(backend=None):
+    """One process per GPU (torch.distributed.run env); returns (world, rank, local, dist or None).
+    The default backend is RCCL ("nccl") on a GPU box; tests pass "gloo"."""
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world == 1:
+        return world, rank, local, None
+    import torch.distributed as dist
+    backend = backend or "nccl"
+    if backend == "nccl":
+        dist.init_process_group(backend, device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group(backend)
+    return world, rank, local, dist
+
+
+def timed_steps(step, steps, warmup, dist=None, sync=lambda: None, device="cuda"):
+    """W untimed warmup steps, then exactly K timed steps bracketed by a barrier + device
+    sync on both sides; returns the MAX elapsed seconds over ranks (every rank gets it)."""
+    import torch
+    for _ in range(warmup):
+        step()
+    sync()
+    if dist is not None:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
+def job_value(units_per_rank, world, elapsed):
+    """Whole-job throughput: the units all ranks processed / the max-over-ranks time."""
+    return units_per_rank * world / elapsed
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -102,14 +149,9 @@ def main():
     args = ap.parse_args()
 
     import torch
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    world, rank, local, dist = init_dist()
 
     import __graft_entry__
     pkg = __graft_entry__.load_package()
@@ -123,28 +165,12 @@ def main():
     s0 = eng.stats()
     eng.set_timing(True)
     eng.timings()
-
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        eng.step()
-    torch.cuda.synchronize()
-    barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = timed_steps(eng.step, args.steps, 0, dist, torch.cuda.synchronize)
     timings = eng.timings()
     s1 = eng.stats()
 
     hands_rank = args.steps * cfg["n_lanes"]
-    value = hands_rank * world / elapsed
+    value = job_value(hands_rank, world, elapsed)
     br_upd = sum(s1["br_updates"]) - sum(s0["br_updates"])
     ar_upd = sum(s1["ar_updates"]) - sum(s0["ar_updates"])
     rl_ins = sum(s1["rl_total"]) - sum(s0["rl_total"])
