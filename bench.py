@@ -229,6 +229,11 @@ def main():
                      "rl_inserts_per_hand": t_rl, "sl_inserts_per_hand": t_sl},
         "exploitability_proxy": sum(s1["exploitability"]),
     }
+    # exact exploitability of the AR nets after the timed steps (outside the timed region)
+    ex = {m: eng.exploitability(m) for m in (0, 1)}
+    out["exploitability_exact"] = {
+        "softmax_mixed": ex[0]["exploitability"], "argmax_as_executed": ex[1]["exploitability"],
+        "hands_trained_per_gpu": int(s1["hands"]), "unit": "chips (BR_0 + BR_1)"}
     if rank == 0 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:

@@ -213,7 +213,7 @@ int nfsp_engine_memories(nfsp_engine* e, int agent, nfsp_records* rl, int64_t* r
 /* Per-kernel timing with HIP events recorded around each launch on the stream it runs on:
  * ms / launches [8] = {k_rollout, k_scan1+k_scan2, k_commit, learner (whole
  * nfsp_engine_update), learner prep (k_br_prep..k_res_apply), k_br_targets,
- * k_chain2<BR>, k_chain2<AR>}, accumulated since the previous nfsp_engine_get_timings
+ * k_chain3<BR>, k_chain3<AR>}, accumulated since the previous nfsp_engine_get_timings
  * (which synchronises and resets them). */
 int nfsp_engine_set_timing(nfsp_engine* e, int on);
 int nfsp_engine_get_timings(nfsp_engine* e, double* ms /*[8]*/, int64_t* launches /*[8]*/);
@@ -221,6 +221,19 @@ int nfsp_engine_get_timings(nfsp_engine* e, double* ms /*[8]*/, int64_t* launche
  * rows [batch] (int64) and fit permutations [epochs][batch] (int32) of its LAST update. */
 int nfsp_engine_last_update(nfsp_engine* e, int agent, int role, int64_t** dev_rows,
                             int32_t** dev_perms);
+
+/* ---- evaluation ----
+ * Exact exploitability of two average-policy nets (packed weights, device pointers; e.g.
+ * nfsp_engine_weights(e, a, 0, ..)) in this Leduc variant as main.train plays it
+ * (main.py:21-67; the reference's proxy is agent/agent.py:235-238 summed at main.py:73,
+ * its MC evaluator main.py:82-120, commented out).  mode 0: each net's softmax as a mixed
+ * strategy (NFSP's average strategy; an illegal raise's mass goes to call); mode 1: the
+ * argmax the env executes (leduc/newenv.py:135-145).  out[0] / out[1]: best-response value
+ * of seat 0 / 1 against the other seat's policy, over both dealers and all deals;
+ * out[2] = out[0] + out[1] (exploitability, chips); out[3] = seat 0's on-policy value.
+ * Synchronises the ctx stream. */
+int nfsp_exploitability(nfsp_ctx* ctx, const float* dev_w_ar0, const float* dev_w_ar1, int mode,
+                        double* out /*[4]*/);
 
 #ifdef __cplusplus
 }

@@ -143,6 +143,11 @@ class SelfPlayEngine:
         return (_wrap_device(rows.value, B, torch.int64, self.dev).cpu().numpy(),
                 _wrap_device(perms.value, E * B, torch.int32, self.dev).view(E, B).cpu().numpy())
 
+    def exploitability(self, mode: int = 0) -> dict:
+        """Exact exploitability of the two agents' current AR nets (nfsp_exploitability):
+        mode 0 = softmax mixed strategies, 1 = the argmax the env executes."""
+        return exploitability(self.ctx, self._wptr(0, NET_AR), self._wptr(1, NET_AR), mode)
+
     def close(self):
         if getattr(self, "h", None):
             self.L.nfsp_engine_destroy(self.h)
@@ -153,6 +158,13 @@ class SelfPlayEngine:
             self.close()
         except Exception:
             pass
+
+
+def exploitability(ctx, dev_w_ar0: int, dev_w_ar1: int, mode: int = 0) -> dict:
+    """nfsp_exploitability on two packed AR nets given as device pointers."""
+    out = (C.c_double * 4)()
+    native.check(ctx.L.nfsp_exploitability(ctx.h, dev_w_ar0, dev_w_ar1, mode, out), "nfsp_exploitability")
+    return {"br0": out[0], "br1": out[1], "exploitability": out[2], "value0": out[3]}
 
 
 def _wrap_device(addr, numel, dtype, device) -> torch.Tensor:

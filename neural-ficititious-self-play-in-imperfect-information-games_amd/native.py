@@ -91,6 +91,7 @@ SIGNATURES = {
     "nfsp_engine_memories": (I32, [P, I32, C.POINTER(Records), C.POINTER(I64), C.POINTER(Records),
                                    PP, PP, PP]),
     "nfsp_engine_last_update": (I32, [P, I32, I32, PP, PP]),
+    "nfsp_exploitability": (I32, [P, P, P, I32, P]),
     "nfsp_engine_set_timing": (I32, [P, I32]),
     "nfsp_engine_get_timings": (I32, [P, C.POINTER(F64), C.POINTER(I64)]),
 }
