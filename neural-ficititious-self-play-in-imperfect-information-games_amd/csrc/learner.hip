@@ -278,47 +278,65 @@ __global__ void __launch_bounds__(256) k_res_apply(PrepArgs P) {
 // ---------------------------------------------------------------------------
 // DQN targets of one BR segment (agent/agent.py:219-241), one update per workgroup
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(128) k_br_targets(LearnBufs LB, const float* __restrict__ tw, int a,
+__global__ void __launch_bounds__(256) k_br_targets(LearnBufs LB, const float* __restrict__ tw, int a,
                                                     int64_t u0, int B, int E, double gamma,
                                                     unsigned quirks, int64_t it0, double lr0) {
+  // threads 0..127: Q_target(s) of row b (waves 0-1); threads 128..255: Q_target(s2) of
+  // row b - 128 (waves 2-3) -- the two forwards of a row run side by side
   __shared__ __attribute__((aligned(16))) float sw[NET_LDS];
   __shared__ float q[MAX_BATCH][3];
   __shared__ float val[MAX_BATCH];
   __shared__ uint32_t sb[MAX_BATCH];
   __shared__ uint8_t am[MAX_BATCH];
-  const int b = threadIdx.x;
-  stage_net_lds(sw, tw, b, blockDim.x);
-  __syncthreads();
+  __shared__ double part[2];
+  __shared__ int lastw[2][3];
+  const int tid = threadIdx.x;
+  const int b = tid & (MAX_BATCH - 1);
+  const bool s2half = tid >= MAX_BATCH;
   const int64_t u = u0 + blockIdx.x;
   const int64_t slot = (int64_t)a * LB.umax + u;
+  BrRow rr{};
+  if (b < B) rr = LB.br_rows[slot * B + b];
+  stage_net_lds(sw, tw, tid, blockDim.x);
+  __syncthreads();
   if (b < B) {
-    const BrRow rr = LB.br_rows[slot * B + b];
-    float qb[3], qn[3];
-    fwd_lds(sw, rr.s, NFSP_ACT_RELU, qb);
-    fwd_lds(sw, rr.s2, NFSP_ACT_RELU, qn);
-    q[b][0] = qb[0]; q[b][1] = qb[1]; q[b][2] = qb[2];
-    const float qmax = fmaxf(fmaxf(qn[0], qn[1]), qn[2]);
-    const float r = (float)(int8_t)((rr.meta >> 16) & 0xFFu) * 0.5f;
-    const bool terminal = !(quirks & NFSP_QUIRK_TERMINAL_BOOTSTRAP) && ((rr.meta >> 8) & 1u);
-    val[b] = (float)(terminal ? (double)r : (double)r + gamma * (double)qmax);
-    am[b] = (uint8_t)(rr.meta & 0xFFu);
-    sb[b] = rr.s;
-  }
-  __syncthreads();
-  if (b == 0) {          // exploitability proxy, before the overwrite (agent/agent.py:235-238)
-    double acc = 0.0;
-    for (int k = 0; k < B; ++k) acc += (double)fmaxf(fmaxf(q[k][0], q[k][1]), q[k][2]);
-    LB.br_expl[slot] = acc / B;
-  }
-  __syncthreads();
-  if (quirks & NFSP_QUIRK_ROW0_TARGET) {
-    if (b < 3) {         // target[0][argmax a_k] = v_k for k = 0..B-1: the last k wins
-      int last = -1;
-      for (int k = 0; k < B; ++k)
-        if (am[k] == b) last = k;
-      if (last >= 0) q[0][b] = val[last];
+    float y[3];
+    if (!s2half) {
+      fwd_lds(sw, rr.s, NFSP_ACT_RELU, y);
+      q[b][0] = y[0]; q[b][1] = y[1]; q[b][2] = y[2];
+      am[b] = (uint8_t)(rr.meta & 0xFFu);
+      sb[b] = rr.s;
+    } else {
+      fwd_lds(sw, rr.s2, NFSP_ACT_RELU, y);
+      const float qmax = fmaxf(fmaxf(y[0], y[1]), y[2]);
+      const float r = (float)(int8_t)((rr.meta >> 16) & 0xFFu) * 0.5f;
+      const bool terminal = !(quirks & NFSP_QUIRK_TERMINAL_BOOTSTRAP) && ((rr.meta >> 8) & 1u);
+      val[b] = (float)(terminal ? (double)r : (double)r + gamma * (double)qmax);
     }
-  } else if (b < B) {
+  }
+  __syncthreads();
+  const int lane = tid & 63, wv = tid >> 6;
+  if (!s2half) {
+    // exploitability proxy (agent/agent.py:235-238): mean of the row maxima, before the
+    // row-0 overwrite; and for the quirk, the last row k with argmax a_k == action
+    double m = b < B ? (double)fmaxf(fmaxf(q[b][0], q[b][1]), q[b][2]) : 0.0;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) m += __shfl_xor(m, off);
+    if (lane == 0) part[wv] = m;
+#pragma unroll
+    for (int act = 0; act < 3; ++act) {
+      const unsigned long long bal = __ballot(b < B && am[b] == act);
+      if (lane == 0) lastw[wv][act] = bal ? 64 * wv + 63 - __builtin_clzll(bal) : -1;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) LB.br_expl[slot] = (part[0] + part[1]) / B;
+  if (quirks & NFSP_QUIRK_ROW0_TARGET) {
+    if (tid < 3) {       // target[0][argmax a_k] = v_k for k = 0..B-1: the last k wins
+      const int last = lastw[1][tid] >= 0 ? lastw[1][tid] : lastw[0][tid];
+      if (last >= 0) q[0][tid] = val[last];
+    }
+  } else if (!s2half && b < B) {
     q[b][am[b]] = val[b];
   }
   __syncthreads();
@@ -328,7 +346,7 @@ __global__ void __launch_bounds__(128) k_br_targets(LearnBufs LB, const float* _
   for (int e = 0; e < E; ++e) {
     uint32_t x = 0;
     float t0 = 0.f, t1 = 0.f, t2 = 0.f;
-    if (b < B) {
+    if (!s2half && b < B) {
       const int k = LB.br_perm[(slot * E + e) * B + b];
       x = sb[k];
       t0 = q[k][0]; t1 = q[k][1]; t2 = q[k][2];
@@ -550,10 +568,11 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
       const float4 q = sm.w2t[w][4 * g + r];
       W2h[r][0] = q.x; W2h[r][1] = q.y; W2h[r][2] = q.z; b1h[r] = q.w;
     }
+    // Z1^T first (layer 2 waits on it); Z1 (needed only by the backward) is issued after
+    // layer 2, so its matrix-core time overlaps the barrier wait
     const floatx4 zh0 = mfma3t(whi, wmid, wlo, fa0);     // Z1^T: hidden 16w+4g+r, sample c
     const floatx4 zh1 = mfma3t(whi, wmid, wlo, fa1);     //                      sample 16+c
-    const floatx4 zs0 = mfma3(fa0, whi, wmid, wlo);      // Z1: sample 4g+r, hidden 16w+c
-    const floatx4 zs1 = mfma3(fa1, whi, wmid, wlo);      //     sample 16+4g+r
+    __builtin_amdgcn_sched_barrier(0);
     CHAIN_STAMP(0);
     // ---- layer 2 partial over the slice, from Z1^T
     float p0[3], p1[3];
@@ -578,6 +597,10 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
     }
     const int buf = t & 1;
     if ((g & 1) == 0) *reinterpret_cast<float4*>(&sm.po[buf][w][sl][0]) = make_float4(q[0], q[1], q[2], 0.f);
+    __builtin_amdgcn_sched_barrier(0);
+    const floatx4 zs0 = mfma3(fa0, whi, wmid, wlo);      // Z1: sample 4g+r, hidden 16w+c
+    const floatx4 zs1 = mfma3(fa1, whi, wmid, wlo);      //     sample 16+4g+r
+    const float4 tg = R.tg[sl];                          // read before the barrier pins it early
     CHAIN_STAMP(1);
     __syncthreads();
     CHAIN_STAMP(2);
@@ -591,7 +614,6 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
       const float o0 = (((a0.x + a1.x) + a2.x) + a3.x) + b2_0;
       const float o1 = (((a0.y + a1.y) + a2.y) + a3.y) + b2_1;
       const float o2 = (((a0.z + a1.z) + a2.z) + a3.z) + b2_2;
-      const float4 tg = R.tg[sl];
       lr_step = tg.w;
       const float tt[3] = {tg.x, tg.y, tg.z};
       if (RELU) {          // Huber on ReLU outputs, mean over 3 x batch
@@ -605,30 +627,28 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
           dd[k] = oz[k] > 0.f ? (-gg * inv3m) : 0.f;
         }
         d0 = dd[0]; d1 = dd[1]; d2 = dd[2];
-      } else {             // Keras categorical cross-entropy on softmax (normalise + clip)
+      } else {
+        // Keras categorical cross-entropy on the softmax (normalise p = y / S, clip p to
+        // [1e-7, 1 - 1e-7], loss -sum t log p; mean over the batch).  Its gradient w.r.t.
+        // the logits in closed form, with M = the unclipped outputs (the clip's gradient
+        // is 0 elsewhere) and T_M = sum_{k in M} t_k:
+        //   d_k = (y_k T_M / S - [k in M] t_k) / batch
+        // (the chain rule through normalise and softmax; the cancelling terms removed --
+        // oracle/nn_oracle.py evaluates the unsimplified chain)
         const float mx = fmaxf(fmaxf(o0, o1), o2);
         const float e0 = __expf(o0 - mx), e1 = __expf(o1 - mx), e2 = __expf(o2 - mx);
         const float rs = __builtin_amdgcn_rcpf((e0 + e1) + e2);
-        const float y[3] = {e0 * rs, e1 * rs, e2 * rs};
-        const float S = (y[0] + y[1]) + y[2];
-        const float rS = __builtin_amdgcn_rcpf(S);
+        const float y0 = e0 * rs, y1 = e1 * rs, y2 = e2 * rs;
+        const float rS = __builtin_amdgcn_rcpf((y0 + y1) + y2);
         const float eps = 1e-7f, hi = 1.0f - 1e-7f;
-        float dp[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          const float pk = y[k] * rS;
-          const float pc = fminf(fmaxf(pk, eps), hi);
-          const float msk = (pk >= eps && pk <= hi) ? invm : 0.f;
-          dp[k] = -(tt[k] * __builtin_amdgcn_rcpf(pc)) * msk;
-        }
-        const float dpy = (dp[0] * y[0] + dp[1] * y[1]) + dp[2] * y[2];
-        float dy[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) dy[k] = (dp[k] - dpy * rS) * rS;
-        const float dyy = (dy[0] * y[0] + dy[1] * y[1]) + dy[2] * y[2];
-        d0 = y[0] * (dy[0] - dyy);
-        d1 = y[1] * (dy[1] - dyy);
-        d2 = y[2] * (dy[2] - dyy);
+        const float q0 = y0 * rS, q1 = y1 * rS, q2 = y2 * rS;
+        const float m0 = (q0 >= eps && q0 <= hi) ? tt[0] : 0.f;
+        const float m1 = (q1 >= eps && q1 <= hi) ? tt[1] : 0.f;
+        const float m2 = (q2 >= eps && q2 <= hi) ? tt[2] : 0.f;
+        const float k = ((m0 + m1) + m2) * rS;
+        d0 = (y0 * k - m0) * invm;
+        d1 = (y1 * k - m1) * invm;
+        d2 = (y2 * k - m2) * invm;
       }
     }
     if ((g & 1) == 0) {
@@ -922,7 +942,7 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
       }
       {
         KTimer kt2(e, KT_TARGETS, sa);
-        k_br_targets<<<(unsigned)(v - u), 128, 0, sa>>>(e->LB, wtg, a, u, cfg.batch, cfg.epochs,
+        k_br_targets<<<(unsigned)(v - u), 256, 0, sa>>>(e->LB, wtg, a, u, cfg.batch, cfg.epochs,
                                                          cfg.gamma, cfg.quirks, it0, cfg.lr_br);
       }
       NFSP_LAUNCHED("k_br_targets");

@@ -3,7 +3,7 @@
 // split of waves 0..3 (s_memtime).  Mode "compare" checks k_chain3 against the previous
 // f32-MFMA chain (tools/chain_ref.hip) from the same start.  Not part of libnfsp.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude -I<pkg>/csrc tools/bench_chain.hip
-//   ./bench_chain <updates> <relu 0|1> [time|compare] [blocks 1|2]
+//   ./bench_chain <updates> <relu 0|1> [time|compare] [blocks 1|2] [layer-2 weight scale]
 #include <math.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -37,6 +37,8 @@ int main(int argc, char** argv) {
   const int relu = argc > 2 ? atoi(argv[2]) : 1;
   const bool compare = argc > 3 && !strcmp(argv[3], "compare");
   const int nblk = argc > 4 ? atoi(argv[4]) : 1;     // concurrent chains (as the AR launch: 2)
+  const float wscale = argc > 5 ? (float)atof(argv[5]) : 1.f;   // e.g. 60: saturated softmax,
+                                                                // exercises the CE clip
   const int B = 128, E = 2, NMB = B / 32;
   std::mt19937 rng(7);
   std::vector<chainref::FitRow> fit((size_t)U * E * B);
@@ -51,6 +53,7 @@ int main(int argc, char** argv) {
   std::vector<float> w(nn::NP);
   std::uniform_real_distribution<float> ud(-0.2f, 0.2f);
   for (auto& v : w) v = ud(rng);
+  for (int i = nn::OW2; i < nn::NP; ++i) w[i] *= wscale;
   // step records, as k_br_targets / k_ar_prep emit them
   std::vector<StepRec> rec((size_t)U * E * NMB);
   for (size_t st = 0; st < rec.size(); ++st) {
