@@ -601,6 +601,7 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
     const floatx4 zs0 = mfma3(fa0, whi, wmid, wlo);      // Z1: sample 4g+r, hidden 16w+c
     const floatx4 zs1 = mfma3(fa1, whi, wmid, wlo);      //     sample 16+4g+r
     const float4 tg = R.tg[sl];                          // read before the barrier pins it early
+    __builtin_amdgcn_sched_barrier(0);                   // ... and the Z1 MFMAs issue before it
     CHAIN_STAMP(1);
     __syncthreads();
     CHAIN_STAMP(2);
@@ -645,10 +646,10 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
         const float m0 = (q0 >= eps && q0 <= hi) ? tt[0] : 0.f;
         const float m1 = (q1 >= eps && q1 <= hi) ? tt[1] : 0.f;
         const float m2 = (q2 >= eps && q2 <= hi) ? tt[2] : 0.f;
-        const float k = ((m0 + m1) + m2) * rS;
-        d0 = (y0 * k - m0) * invm;
-        d1 = (y1 * k - m1) * invm;
-        d2 = (y2 * k - m2) * invm;
+        const float k = ((m0 + m1) + m2) * (rS * invm);
+        d0 = y0 * k - m0 * invm;
+        d1 = y1 * k - m1 * invm;
+        d2 = y2 * k - m2 * invm;
       }
     }
     if ((g & 1) == 0) {
