@@ -216,6 +216,14 @@ int nfsp_engine_memories(nfsp_engine* e, int agent, nfsp_records* rl, int64_t* r
  * k_chain3<BR>, k_chain3<AR>}, accumulated since the previous nfsp_engine_get_timings
  * (which synchronises and resets them). */
 int nfsp_engine_set_timing(nfsp_engine* e, int on);
+/* Loss log (observability; the reference's TensorBoard callbacks on fit, agent/agent.py:
+ * 84-88,243,264): when on, the SGD chains also record each update's Keras epoch losses
+ * (BR: the py2 huber_loss of agent/agent.py:91-99, where 1 / 2 == 0; AR: categorical
+ * cross-entropy), each minibatch's loss taken before its step.  nfsp_engine_losses gives, per
+ * agent a and net n (0 = AR, 1 = BR), out[(2a + n) * 2 + 0] = the mean epoch loss over the last
+ * nfsp_engine_update's updates and [.. + 1] = its last update's final-epoch loss (NaN: none). */
+int nfsp_engine_set_loss_log(nfsp_engine* e, int on);
+int nfsp_engine_losses(nfsp_engine* e, double* out /*[2][2][2]*/);
 int nfsp_engine_get_timings(nfsp_engine* e, double* ms /*[8]*/, int64_t* launches /*[8]*/);
 /* Debug view of the last learner run: per agent and role (0 = AR, 1 = BR) the sampled
  * rows [batch] (int64) and fit permutations [epochs][batch] (int32) of its LAST update. */

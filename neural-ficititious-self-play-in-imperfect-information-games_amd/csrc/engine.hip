@@ -17,6 +17,9 @@
 //               AR workgroup applies the reservoir inserts in stream order in between.
 #include <math.h>
 
+#include <cmath>
+#include <vector>
+
 #include "engine_internal.h"
 
 using nfsp::Hand;
@@ -443,6 +446,8 @@ extern "C" int nfsp_engine_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, nfs
   EALLOC(L.br_rec, sizeof(StepRec) * (ueb / CHAIN_MB));
   EALLOC(L.ar_rec, sizeof(StepRec) * (ueb / CHAIN_MB));
   EALLOC(L.ar_active, 2 * L.umax);
+  EALLOC(L.br_loss, 4 * 2 * L.umax * cfg->epochs);
+  EALLOC(L.ar_loss, 4 * 2 * L.umax * cfg->epochs);
   EALLOC(L.res_head, sizeof(unsigned long long) * sc);
   EALLOC(L.res_next, 4 * pc);
   EALLOC(L.res_slot, 4 * pc);
@@ -592,6 +597,33 @@ extern "C" int nfsp_engine_last_update(nfsp_engine* e, int agent, int role, int6
 extern "C" int nfsp_engine_set_timing(nfsp_engine* e, int on) {
   NFSP_REQUIRE(e, "null argument");
   e->timing = on != 0;
+  return NFSP_OK;
+}
+
+extern "C" int nfsp_engine_set_loss_log(nfsp_engine* e, int on) {
+  NFSP_REQUIRE(e, "null argument");
+  e->log_loss = on != 0;
+  return NFSP_OK;
+}
+
+extern "C" int nfsp_engine_losses(nfsp_engine* e, double* out) {
+  NFSP_REQUIRE(e && out, "null argument");
+  NFSP_REQUIRE(e->log_loss, "the loss log is off (nfsp_engine_set_loss_log)");
+  NFSP_HIP(hipStreamSynchronize(e->ctx->stream));
+  const int E = e->cfg.epochs;
+  for (int a = 0; a < 2; ++a)
+    for (int n = 0; n < 2; ++n) {                 // n: 0 = AR (avg_strategy_model), 1 = BR
+      const int64_t U = n ? e->last_Ubr[a] : e->last_U[a];
+      const float* src = (n ? e->LB.br_loss : e->LB.ar_loss) + (int64_t)a * e->LB.umax * E;
+      std::vector<float> h((size_t)(U * E));
+      if (U > 0) NFSP_HIP(hipMemcpy(h.data(), src, sizeof(float) * U * E, hipMemcpyDeviceToHost));
+      double sum = 0.0, last = NAN;
+      int64_t cnt = 0;
+      for (int64_t q = 0; q < U * E; ++q)
+        if (!std::isnan(h[q])) { sum += h[q]; cnt++; last = h[q]; }
+      out[(a * 2 + n) * 2 + 0] = cnt ? sum / (double)cnt : NAN;
+      out[(a * 2 + n) * 2 + 1] = last;
+    }
   return NFSP_OK;
 }
 

@@ -95,6 +95,8 @@ struct LearnBufs {
   double* br_expl;     // [2][umax]
   StepRec* br_rec;     // [2][umax][epochs][batch / 32]: one record per SGD step
   StepRec* ar_rec;     // [2][umax][epochs][batch / 32]
+  float* br_loss;      // [2][umax][epochs] Keras epoch losses when the loss log is on (NaN:
+  float* ar_loss;      //   no fit), the values agent/agent.py:243,264's TensorBoard logs
   uint8_t* ar_active;  // [2][umax]
   unsigned long long* res_head;   // [2][sl_cap]  (tag << 32 | q)
   int32_t* res_next;   // [2][pend_cap]
@@ -187,6 +189,8 @@ struct nfsp_engine {
   std::vector<void*> allocs;
   // optional per-kernel timing: (kernel id, start, stop) event triples on the ctx stream
   bool timing = false;
+  bool log_loss = false;
+  int64_t last_U[2] = {0, 0}, last_Ubr[2] = {0, 0};   // the last learner call's update counts
   std::vector<hipEvent_t> pool;
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> marks;
 };

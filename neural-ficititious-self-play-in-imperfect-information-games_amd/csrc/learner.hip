@@ -370,6 +370,8 @@ struct ChainArgs {
   int agents[2];                  // blockIdx -> agent
   int B, E;
   unsigned long long* stamps;     // diagnostic build only (NFSP_CHAIN_STAMPS): phase cycles
+  float* loss_out;                // optional: [2][umax][E] Keras epoch losses (the values the
+                                  // reference's TensorBoard callbacks log, agent/agent.py:84-88)
 };
 
 // In-kernel phase stamps (cdna_hip_programming.md §7): a separate diagnostic build only.
@@ -488,7 +490,7 @@ __device__ inline floatx4 mfma3t(bf16x8 ahi, bf16x8 amid, bf16x8 alo, bf16x8 b) 
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, b, z, 0, 0, 0);
 }
 
-template <int RELU>
+template <int RELU, int LOSS>
 __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   Chain3Smem& sm = *reinterpret_cast<Chain3Smem*>(smem_raw);
@@ -551,6 +553,7 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
   // record t + 2 and stores it at the end of step t; barrier(t + 1) publishes it.  Every
   // load is consumed inside its own step (nothing loop-carried in registers), and the 4
   // waves share one copy of each record.
+  float loss_acc = 0.f;                        // wave 0 lane 0: running epoch loss
   auto step = [&]() {
     uint4 va, vb;
     issue(t + 2, va, vb);
@@ -607,6 +610,7 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
     CHAIN_STAMP(2);
     // ---- output + loss of sample sl (every wave redundantly, identical results)
     float d0, d1, d2, lr_step;
+    float o_keep[3], tt_keep[3], p_keep[3];     // for the optional loss log
     {
       const float4 a0 = *reinterpret_cast<const float4*>(&sm.po[buf][0][sl][0]);
       const float4 a1 = *reinterpret_cast<const float4*>(&sm.po[buf][1][sl][0]);
@@ -617,6 +621,8 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
       const float o2 = (((a0.z + a1.z) + a2.z) + a3.z) + b2_2;
       lr_step = tg.w;
       const float tt[3] = {tg.x, tg.y, tg.z};
+      o_keep[0] = o0; o_keep[1] = o1; o_keep[2] = o2;
+      tt_keep[0] = tg.x; tt_keep[1] = tg.y; tt_keep[2] = tg.z;
       if (RELU) {          // Huber on ReLU outputs, mean over 3 x batch
         const float oz[3] = {o0, o1, o2};
         float dd[3];
@@ -643,6 +649,7 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
         const float rS = __builtin_amdgcn_rcpf((y0 + y1) + y2);
         const float eps = 1e-7f, hi = 1.0f - 1e-7f;
         const float q0 = y0 * rS, q1 = y1 * rS, q2 = y2 * rS;
+        p_keep[0] = q0; p_keep[1] = q1; p_keep[2] = q2;
         const float m0 = (q0 >= eps && q0 <= hi) ? tt[0] : 0.f;
         const float m1 = (q1 >= eps && q1 <= hi) ? tt[1] : 0.f;
         const float m2 = (q2 >= eps && q2 <= hi) ? tt[2] : 0.f;
@@ -650,6 +657,36 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
         d0 = y0 * k - m0 * invm;
         d1 = y1 * k - m1 * invm;
         d2 = y2 * k - m2 * invm;
+      }
+    }
+    if (LOSS) {            // fit loss of this minibatch (before its update), Keras' epoch mean
+      float Ls;
+      if (RELU) {          // huber_loss with py2's 1 / 2 == 0: |e| > 1 ? |e| : e^2 / 2, mean over 3
+        float acc = 0.f;
+        for (int k = 0; k < 3; ++k) {
+          const float e = tt_keep[k] - fmaxf(o_keep[k], 0.f);
+          acc += fabsf(e) > 1.0f ? fabsf(e) : 0.5f * e * e;
+        }
+        Ls = acc * (1.0f / 3.0f);
+      } else {             // categorical cross-entropy: -sum t log(clip(y / S))
+        float acc = 0.f;
+        for (int k = 0; k < 3; ++k) acc -= tt_keep[k] * __logf(fminf(fmaxf(p_keep[k], 1e-7f), 1.0f - 1e-7f));
+        Ls = acc;
+      }
+      float x = (g & 1) == 0 ? Ls : 0.f;     // the 32 distinct samples: rows 0 and 2
+      x = x + dpp_any(x, 0x128);
+      x = x + dpp_any(x, 0x124);
+      x = x + dpp_any(x, 0x122);
+      x = x + dpp_any(x, 0x121);
+      x = sum_x32(sum_x16(x));
+      if (w == 0 && l == 0) {
+        const int in_u = t % spu;
+        loss_acc += x * invm;
+        if (in_u % nmb == nmb - 1) {
+          const int64_t uu = t / spu, ee = in_u / nmb;
+          C.loss_out[(slot0 + uu) * C.E + ee] = loss_acc / (float)nmb;
+          loss_acc = 0.f;
+        }
       }
     }
     if ((g & 1) == 0) {
@@ -878,11 +915,20 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
   }
   static bool attr = false;
   if (!attr) {
-    NFSP_HIP(hipFuncSetAttribute((const void*)k_chain3<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 CHAIN_LDS));
-    NFSP_HIP(hipFuncSetAttribute((const void*)k_chain3<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 CHAIN_LDS));
+    for (const void* f : {(const void*)k_chain3<0, 0>, (const void*)k_chain3<1, 0>, (const void*)k_chain3<0, 1>,
+                          (const void*)k_chain3<1, 1>})
+      NFSP_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, CHAIN_LDS));
     attr = true;
+  }
+  for (int a = 0; a < 2; ++a) {
+    e->last_U[a] = P.A[a].U;
+    e->last_Ubr[a] = P.A[a].U_br;
+    if (e->log_loss) {       // NaN = no fit recorded (inactive AR update)
+      NFSP_HIP(hipMemsetAsync(e->LB.ar_loss + a * e->LB.umax * cfg.epochs, 0xFF,
+                              sizeof(float) * P.A[a].U * cfg.epochs, s));
+      NFSP_HIP(hipMemsetAsync(e->LB.br_loss + a * e->LB.umax * cfg.epochs, 0xFF,
+                              sizeof(float) * P.A[a].U_br * cfg.epochs, s));
+    }
   }
   hipEvent_t fork = take_event(e);
   NFSP_HIP(hipEventRecord(fork, s));
@@ -891,6 +937,7 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
     NFSP_HIP(hipStreamWaitEvent(e->s_ar, fork, 0));
     ChainArgs C{};
     C.rec = e->LB.ar_rec;
+    C.loss_out = e->log_loss ? e->LB.ar_loss : nullptr;
     C.active = e->LB.ar_active;
     C.umax = e->LB.umax;
     C.B = cfg.batch;
@@ -903,7 +950,8 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
       C.u1[a] = P.A[a].U;
     }
     KTimer kc(e, KT_CHAIN_AR, e->s_ar);
-    k_chain3<0><<<2, 256, CHAIN_LDS, e->s_ar>>>(C);
+    if (C.loss_out) k_chain3<0, 1><<<2, 256, CHAIN_LDS, e->s_ar>>>(C);
+    else k_chain3<0, 0><<<2, 256, CHAIN_LDS, e->s_ar>>>(C);
     NFSP_LAUNCHED("k_chain(AR)");
   }
   // diagnostic (NFSP_LEARNER_SERIAL=1): BR work waits for the AR chains, to time them alone
@@ -949,6 +997,7 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
       NFSP_LAUNCHED("k_br_targets");
       ChainArgs C{};
       C.rec = e->LB.br_rec;
+      C.loss_out = e->log_loss ? e->LB.br_loss : nullptr;
       C.active = nullptr;
       C.umax = e->LB.umax;
       C.B = cfg.batch;
@@ -960,7 +1009,8 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
       C.u1[0] = v;
       {
         KTimer kc(e, KT_CHAIN_BR, sa);
-        k_chain3<1><<<1, 256, CHAIN_LDS, sa>>>(C);
+        if (C.loss_out) k_chain3<1, 1><<<1, 256, CHAIN_LDS, sa>>>(C);
+        else k_chain3<1, 0><<<1, 256, CHAIN_LDS, sa>>>(C);
       }
       NFSP_LAUNCHED("k_chain(BR)");
       u = v;

@@ -143,6 +143,24 @@ class SelfPlayEngine:
         return (_wrap_device(rows.value, B, torch.int64, self.dev).cpu().numpy(),
                 _wrap_device(perms.value, E * B, torch.int32, self.dev).view(E, B).cpu().numpy())
 
+    loss_log = False
+
+    def set_loss_log(self, on=True):
+        native.check(self.L.nfsp_engine_set_loss_log(self.h, int(bool(on))), "set_loss_log")
+        self.loss_log = bool(on)
+
+    def losses(self) -> dict:
+        """Keras epoch losses of the last learner call (nfsp_engine_losses), keyed like the
+        reference's TensorBoard log dirs (agent/agent.py:84-88): Player{a}rl = BR, Player{a}sl = AR."""
+        out = (C.c_double * 8)()
+        native.check(self.L.nfsp_engine_losses(self.h, out), "nfsp_engine_losses")
+        d = {}
+        for a in (0, 1):
+            for n, tag in ((0, "sl"), (1, "rl")):
+                d[f"Player{a}{tag}/loss_mean"] = out[(2 * a + n) * 2]
+                d[f"Player{a}{tag}/loss_last"] = out[(2 * a + n) * 2 + 1]
+        return d
+
     def exploitability(self, mode: int = 0) -> dict:
         """Exact exploitability of the two agents' current AR nets (nfsp_exploitability):
         mode 0 = softmax mixed strategies, 1 = the argmax the env executes."""

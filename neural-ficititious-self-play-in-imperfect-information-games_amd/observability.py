@@ -1,0 +1,65 @@
+"""Observability: the reference's scalar outputs for the batched engine.
+
+The reference reports through three channels, and each has an equivalent here:
+
+* ``sampled_actions`` (agent/agent.py:196-204) prints per-agent action counts and rewards.
+  The engine's counterpart is ``nfsp_engine_stats``' ``actions`` and ``reward`` fields (the
+  drop-in ``Agent.sampled_actions`` keeps the reference's print).
+* TensorBoard callbacks on every ``fit`` (agent/agent.py:84-88,243,264) log the epoch loss
+  under ``./logs/<name>rl`` (BR) and ``./logs/<name>sl`` (AR).  The engine's loss log
+  (``SelfPlayEngine.set_loss_log``) gives the same values; TensorBoard itself is not in the
+  image, so they are written as JSON lines with the same tags.
+* The exploitability proxy is printed and plotted (main.py:71-75,122-123).  It is logged
+  here beside the exact exploitability (``nfsp_exploitability``).
+"""
+from __future__ import annotations
+
+import json
+import time
+
+
+class ScalarLog:
+    """One JSON object per line: ``{"step": k, "wall_s": t, <tag>: value, ...}``."""
+
+    def __init__(self, path: str):
+        self.f = open(path, "a", buffering=1)
+        self.t0 = time.perf_counter()
+
+    def write(self, step: int, **scalars):
+        rec = {"step": int(step), "wall_s": round(time.perf_counter() - self.t0, 6)}
+        rec.update({k: (float(v) if isinstance(v, (int, float)) else v) for k, v in scalars.items()})
+        self.f.write(json.dumps(rec) + "\n")
+
+    def close(self):
+        self.f.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def engine_scalars(eng, exact: bool = False) -> dict:
+    """The scalars of one engine step, tagged like the reference's outputs."""
+    st = eng.stats()
+    out = {"hands": int(st["hands"]),
+           "exploitability_proxy": float(sum(st["exploitability"]))}       # main.py:73
+    for a in (0, 1):
+        name = f"Player{a}"
+        acts = st["actions"][a]
+        out[f"{name}/folds"], out[f"{name}/calls"], out[f"{name}/raises"] = (int(x) for x in acts)
+        out[f"{name}/reward"] = float(st["reward"][a])
+        out[f"{name}/epsilon"] = float(st["epsilon"][a])
+        out[f"{name}/lr_br"] = float(st["lr_br"][a])
+        out[f"{name}/temp"] = float(st["temp"][a])
+        out[f"{name}/iteration"] = int(st["iteration"][a])
+        out[f"{name}/br_updates"] = int(st["br_updates"][a])
+        out[f"{name}/ar_updates"] = int(st["ar_updates"][a])
+        out[f"{name}/proxy"] = float(st["exploitability"][a])
+    if getattr(eng, "loss_log", False):
+        out.update(eng.losses())
+    if exact:
+        for m, tag in ((0, "softmax"), (1, "argmax")):
+            out[f"exploitability_exact_{tag}"] = eng.exploitability(m)["exploitability"]
+    return out

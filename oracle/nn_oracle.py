@@ -137,6 +137,22 @@ class MLP:
         gb1 = dz1.sum(axis=0)
         return gW1.astype(F32), gb1.astype(F32), gW2.astype(F32), gb2.astype(F32)
 
+    def loss(self, x2d: np.ndarray, t2d: np.ndarray) -> float:
+        """The Keras loss value of one minibatch (what the TensorBoard callbacks log,
+        agent/agent.py:84-88,243,264): BR huber_loss as the reference runs it under py2
+        (agent/agent.py:91-99: ``1 / 2 == 0``, so the linear term is |e|), mean over the 3
+        outputs then the batch; AR categorical cross-entropy on the normalised, clipped
+        softmax, mean over the batch."""
+        y = self._forward(x2d)[3].astype(np.float64)
+        t = t2d.astype(np.float64)
+        if self.act == ACT_RELU:
+            e = t - y
+            v = np.where(np.abs(e) > 1.0, np.abs(e), 0.5 * e * e)
+            return float(v.mean(axis=-1).mean())
+        p = y / y.sum(axis=-1, keepdims=True)
+        pc = np.clip(p, float(CE_EPS), 1.0 - float(CE_EPS))
+        return float((-(t * np.log(pc)).sum(axis=-1)).mean())
+
     def sgd_step(self, x2d, t2d, lr):
         gW1, gb1, gW2, gb2 = self.grads(x2d, t2d)
         lr = F32(lr)
@@ -145,7 +161,8 @@ class MLP:
         self.W2 = (self.W2 - lr * gW2).astype(F32)
         self.b2 = (self.b2 - lr * gb2).astype(F32)
 
-    def fit(self, x, t, lr, epochs: int = 2, batch_size: int = 32, shuffle_rng=None, perms=None):
+    def fit(self, x, t, lr, epochs: int = 2, batch_size: int = 32, shuffle_rng=None, perms=None,
+            epoch_losses=None):
         """Keras 2.x ``fit_loop``: per epoch ``np.random.shuffle(index_array)``, then
         consecutive slices of ``batch_size``, one SGD step each.
 
@@ -164,9 +181,14 @@ class MLP:
                 idx = np.arange(n)
                 (shuffle_rng if shuffle_rng is not None else np.random).shuffle(idx)
             used.append(idx.copy())
+            ls = []
             for b0 in range(0, n, batch_size):
                 sel = idx[b0:b0 + batch_size]
+                if epoch_losses is not None:          # Keras: batch loss before its update
+                    ls.append(self.loss(x2d[sel], t2d[sel]))
                 self.sgd_step(x2d[sel], t2d[sel], lr)
+            if epoch_losses is not None:
+                epoch_losses.append(float(np.mean(ls)))
         return np.stack(used)
 
 

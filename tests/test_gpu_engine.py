@@ -95,8 +95,10 @@ def test_learner_first_updates_match_oracle(pkg):
     eng.rollout()
     mem = [eng.memories(a) for a in (0, 1)]
     logs = [{k: v.cpu().numpy().copy() for k, v in m.items() if torch.is_tensor(v)} for m in mem]
+    eng.set_loss_log(True)
     eng.update()
     st = eng.stats()
+    losses = eng.losses()
     for a in (0, 1):
         L = logs[a]
         # ---- BR: targets from the (initial) target net, Huber fit, schedules
@@ -114,9 +116,13 @@ def test_learner_first_updates_match_oracle(pkg):
         expl = float(np.mean(target.max(axis=1).astype(np.float64)))
         for k in range(128):
             target[0][int(np.argmax(act[k]))] = vals[k]    # row-0 quirk
-        br.fit(s, target, np.float32(0.05), perms=perms)
+        ep_br = []
+        br.fit(s, target, np.float32(0.05), perms=perms, epoch_losses=ep_br)
         got = eng.get_weights(a, 1)
         assert np.abs(got - br.flat()).max() <= 1e-5
+        # loss log (the TensorBoard scalars of agent/agent.py:243): Keras epoch losses
+        assert losses[f"Player{a}rl/loss_last"] == pytest.approx(ep_br[-1], abs=1e-5)
+        assert losses[f"Player{a}rl/loss_mean"] == pytest.approx(np.mean(ep_br), abs=1e-5)
         assert np.abs(eng.get_weights(a, 2) - got).max() == 0     # first update syncs
         assert st["iteration"][a] == 2 and st["br_updates"][a] == 1
         assert st["epsilon"][a] == pytest.approx(0.06 / 2)
@@ -135,8 +141,11 @@ def test_learner_first_updates_match_oracle(pkg):
                           for v in L["pend_x"][:k_sl].astype(np.uint32)[rows_ar]], np.float32)
             y = L["pend_a"][:k_sl][rows_ar]
             ar = nn.MLP(nn.ACT_SOFTMAX, 64, weights=nn.unpack_weights(w0[(a, 0)]))
-            ar.fit(x, y, np.float32(0.1), perms=perms_ar)
+            ep_ar = []
+            ar.fit(x, y, np.float32(0.1), perms=perms_ar, epoch_losses=ep_ar)
             assert np.abs(eng.get_weights(a, 0) - ar.flat()).max() <= 1e-5
+            assert losses[f"Player{a}sl/loss_last"] == pytest.approx(ep_ar[-1], abs=1e-5)
+            assert losses[f"Player{a}sl/loss_mean"] == pytest.approx(np.mean(ep_ar), abs=1e-5)
         else:
             assert st["ar_updates"][a] == 0
         assert st["sl_size"][a] == min(k_sl, 40000)

@@ -1,0 +1,33 @@
+"""Observability: the scalar log and the engine scalars with the reference's tags."""
+import json
+
+import numpy as np
+import pytest
+
+
+def test_scalar_log_jsonl(pkg, tmp_path):
+    obs = pkg.observability
+    p = tmp_path / "log.jsonl"
+    with obs.ScalarLog(str(p)) as log:
+        log.write(0, **{"Player0rl/loss_mean": 0.5, "hands": 3})
+        log.write(1, **{"Player0rl/loss_mean": np.float32(0.25)})
+    rows = [json.loads(l) for l in p.read_text().splitlines()]
+    assert [r["step"] for r in rows] == [0, 1]
+    assert rows[1]["Player0rl/loss_mean"] == pytest.approx(0.25)
+    assert all("wall_s" in r for r in rows)
+
+
+@pytest.mark.gpu
+def test_engine_scalars_tags(pkg):
+    eng = pkg.engine.SelfPlayEngine(n_lanes=4096, rl_capacity=40_000, sl_capacity=40_000, seed=5)
+    eng.set_loss_log(True)
+    for _ in range(3):
+        eng.step()
+    sc = pkg.observability.engine_scalars(eng, exact=True)
+    for a in (0, 1):
+        for tag in ("rl", "sl"):
+            v = sc[f"Player{a}{tag}/loss_mean"]
+            assert np.isfinite(v) and v >= 0
+        assert sc[f"Player{a}/folds"] + sc[f"Player{a}/calls"] + sc[f"Player{a}/raises"] > 0
+    assert sc["hands"] == 3 * 4096
+    assert sc["exploitability_exact_softmax"] >= 0

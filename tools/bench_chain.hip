@@ -87,11 +87,11 @@ int main(int argc, char** argv) {
   chainref::RefArgs R{};
   R.w[0] = dw; R.fit = dfit; R.umax = U; R.u0[0] = 0; R.u1[0] = U; R.B = B; R.E = E;
   R.lr_fixed = 0.1f; R.lr0 = 0.05;
-  CK(hipFuncSetAttribute((const void*)k_chain3<0>, hipFuncAttributeMaxDynamicSharedMemorySize, CHAIN_LDS));
-  CK(hipFuncSetAttribute((const void*)k_chain3<1>, hipFuncAttributeMaxDynamicSharedMemorySize, CHAIN_LDS));
+  CK(hipFuncSetAttribute((const void*)k_chain3<0, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, CHAIN_LDS));
+  CK(hipFuncSetAttribute((const void*)k_chain3<1, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, CHAIN_LDS));
   auto launch3 = [&]() {
-    if (relu) k_chain3<1><<<nblk, 256, CHAIN_LDS>>>(C);
-    else k_chain3<0><<<nblk, 256, CHAIN_LDS>>>(C);
+    if (relu) k_chain3<1, 0><<<nblk, 256, CHAIN_LDS>>>(C);
+    else k_chain3<0, 0><<<nblk, 256, CHAIN_LDS>>>(C);
   };
   if (compare) {
     std::vector<float> out[2];
