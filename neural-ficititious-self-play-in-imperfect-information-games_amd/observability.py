@@ -27,7 +27,8 @@ class ScalarLog:
 
     def write(self, step: int, **scalars):
         rec = {"step": int(step), "wall_s": round(time.perf_counter() - self.t0, 6)}
-        rec.update({k: (float(v) if isinstance(v, (int, float)) else v) for k, v in scalars.items()})
+        for k, v in scalars.items():            # numpy scalars included
+            rec[k] = v.item() if hasattr(v, "item") else v
         self.f.write(json.dumps(rec) + "\n")
 
     def close(self):
