@@ -202,11 +202,15 @@ int nfsp_rollout(nfsp_engine* e);
 int nfsp_engine_update(nfsp_engine* e);
 int nfsp_engine_step(nfsp_engine* e);          /* nfsp_rollout + nfsp_engine_update */
 int nfsp_engine_get_stats(nfsp_engine* e, nfsp_engine_stats* out);   /* synchronises */
-/* Views of agent's memories: M_RL is a circular log of rl_log_cap rows whose record k
+/* Agent's memories in the reference's fp32 tuple layout (utils/replay_buffer.py:53-57),
+ * expanded on the ctx stream at the call from the packed device records (M_RL: 32 B
+ * {s bits, s2 bits, argmax|t|r, a[3]}, M_SL: 16 B {bits, a[3]}; the export buffers are
+ * allocated on first use).  M_RL is a circular log of rl_log_cap rows whose record k
  * (k-th insert ever) sits at row k % rl_log_cap; the logical M_RL is the last
  * min(rl_total, rl_capacity) records.  sl: the reservoir (rows [0, sl_size)).
- * pending_sl: the last rollout's M_SL records not yet applied by nfsp_engine_update,
- * in insert order, with rl_pos = the agent's RL insert count when each was made. */
+ * pending_sl (live views): the last rollout's M_SL records not yet applied by
+ * nfsp_engine_update, in insert order, with rl_pos = the agent's RL insert count when each
+ * was made. */
 int nfsp_engine_memories(nfsp_engine* e, int agent, nfsp_records* rl, int64_t* rl_log_cap,
                          nfsp_records* sl, uint32_t** dev_pending_sl_obs,
                          float** dev_pending_sl_a, int64_t** dev_pending_sl_rl_pos);

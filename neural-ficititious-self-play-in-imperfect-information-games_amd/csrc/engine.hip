@@ -18,6 +18,7 @@
 #include <math.h>
 
 #include <cmath>
+#include <utility>
 #include <vector>
 
 #include "engine_internal.h"
@@ -280,20 +281,16 @@ __global__ void __launch_bounds__(256) k_commit(int N, unsigned quirks, Staging 
     const int p = (meta >> 9) & 1;
     const int64_t pos = st->rl_total[p] + off_rl[p] + seen[p]++;
     const int64_t row = (int64_t)p * M.log_cap + pos % M.log_cap;
-    const uint32_t sb = alias ? S.fin_s[p * N + L] : S.rl_s[k * N + L];
-    const uint32_t s2b = S.rl_s2[k * N + L];
-    float* srow = M.rl_s + row * nfsp::OBS;
-    float* s2row = M.rl_s2 + row * nfsp::OBS;
+    float a[3];
 #pragma unroll
-    for (int f = 0; f < nfsp::OBS; ++f) {
-      srow[f] = (float)((sb >> f) & 1u);
-      s2row[f] = (float)((s2b >> f) & 1u);
-    }
-#pragma unroll
-    for (int c = 0; c < 3; ++c)
-      M.rl_a[row * 3 + c] = alias ? S.fin_a[(p * 3 + c) * N + L] : S.rl_a[(k * 3 + c) * N + L];
-    M.rl_r[row] = (float)(int8_t)(meta & 0xFFu) * 0.5f;
-    M.rl_t[row] = (uint8_t)((meta >> 8) & 1u);
+    for (int c = 0; c < 3; ++c) a[c] = alias ? S.fin_a[(p * 3 + c) * N + L] : S.rl_a[(k * 3 + c) * N + L];
+    RlRec rec;
+    rec.s = alias ? S.fin_s[p * N + L] : S.rl_s[k * N + L];
+    rec.s2 = S.rl_s2[k * N + L];
+    rec.meta = (uint32_t)nfsp::argmax3(a[0], a[1], a[2]) | (meta & 0x100u) | ((meta & 0xFFu) << 16);
+    rec.a0 = a[0]; rec.a1 = a[1]; rec.a2 = a[2];
+    rec.pad[0] = rec.pad[1] = 0;
+    M.rl[row] = rec;
   }
   int sseen[2] = {0, 0};
   for (int k = 0; k < nsl; ++k) {
@@ -304,6 +301,34 @@ __global__ void __launch_bounds__(256) k_commit(int N, unsigned quirks, Staging 
 #pragma unroll
     for (int c = 0; c < 3; ++c) M.pend_a[li * 3 + c] = S.sl_a[(k * 3 + c) * N + L];
     M.pend_pos[li] = st->rl_total[p] + off_rl[p] + (int64_t)(meta >> 8);
+  }
+}
+
+// the reference's fp32 tuple layout (utils/replay_buffer.py:53-57) of agent a's memories
+__global__ void __launch_bounds__(256) k_export_mem(Memories M, int a) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < M.log_cap) {
+    const int64_t row = (int64_t)a * M.log_cap + i;
+    const RlRec r = M.rl[row];
+#pragma unroll
+    for (int f = 0; f < nfsp::OBS; ++f) {
+      M.ex_rl_s[row * nfsp::OBS + f] = (float)((r.s >> f) & 1u);
+      M.ex_rl_s2[row * nfsp::OBS + f] = (float)((r.s2 >> f) & 1u);
+    }
+    M.ex_rl_a[row * 3 + 0] = r.a0;
+    M.ex_rl_a[row * 3 + 1] = r.a1;
+    M.ex_rl_a[row * 3 + 2] = r.a2;
+    M.ex_rl_r[row] = (float)(int8_t)((r.meta >> 16) & 0xFFu) * 0.5f;
+    M.ex_rl_t[row] = (uint8_t)((r.meta >> 8) & 1u);
+  }
+  if (i < M.sl_cap) {
+    const int64_t row = (int64_t)a * M.sl_cap + i;
+    const SlRec r = M.sl[row];
+#pragma unroll
+    for (int f = 0; f < nfsp::OBS; ++f) M.ex_sl_s[row * nfsp::OBS + f] = (float)((r.x >> f) & 1u);
+    M.ex_sl_a[row * 3 + 0] = r.a0;
+    M.ex_sl_a[row * 3 + 1] = r.a1;
+    M.ex_sl_a[row * 3 + 2] = r.a2;
   }
 }
 
@@ -424,13 +449,8 @@ extern "C" int nfsp_engine_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, nfs
   e->M.sl_cap = cfg->sl_capacity;
   e->M.pend_cap = 4 * N;
   const int64_t lc = 2 * e->M.log_cap, sc = 2 * e->M.sl_cap, pc = 2 * e->M.pend_cap;
-  EALLOC(e->M.rl_s, 4 * nfsp::OBS * lc);
-  EALLOC(e->M.rl_s2, 4 * nfsp::OBS * lc);
-  EALLOC(e->M.rl_a, 4 * 3 * lc);
-  EALLOC(e->M.rl_r, 4 * lc);
-  EALLOC(e->M.rl_t, lc);
-  EALLOC(e->M.sl_s, 4 * nfsp::OBS * sc);
-  EALLOC(e->M.sl_a, 4 * 3 * sc);
+  EALLOC(e->M.rl, sizeof(RlRec) * lc);
+  EALLOC(e->M.sl, sizeof(SlRec) * sc);
   EALLOC(e->M.pend_x, 4 * pc);
   EALLOC(e->M.pend_a, 4 * 3 * pc);
   EALLOC(e->M.pend_pos, 8 * pc);
@@ -559,20 +579,36 @@ extern "C" int nfsp_engine_get_stats(nfsp_engine* e, nfsp_engine_stats* out) {
 extern "C" int nfsp_engine_memories(nfsp_engine* e, int agent, nfsp_records* rl, int64_t* log_cap,
                                     nfsp_records* sl, uint32_t** px, float** pa, int64_t** ppos) {
   NFSP_REQUIRE(e && (agent == 0 || agent == 1), "bad argument");
-  const int64_t lo = (int64_t)agent * e->M.log_cap;
-  if (rl) {
-    rl->s = e->M.rl_s + lo * nfsp::OBS;
-    rl->a = e->M.rl_a + lo * 3;
-    rl->r = e->M.rl_r + lo;
-    rl->s2 = e->M.rl_s2 + lo * nfsp::OBS;
-    rl->t = e->M.rl_t + lo;
-    rl->cap = e->M.log_cap;
+  Memories& M = e->M;
+  if ((rl || sl) && !M.ex_rl_s) {      // the fp32 reference-layout views, on first use
+    const int64_t lc = 2 * M.log_cap, sc = 2 * M.sl_cap;
+    for (auto pr : {std::make_pair((void**)&M.ex_rl_s, 4 * nfsp::OBS * lc), std::make_pair((void**)&M.ex_rl_s2, 4 * nfsp::OBS * lc),
+                    std::make_pair((void**)&M.ex_rl_a, 4 * 3 * lc), std::make_pair((void**)&M.ex_rl_r, 4 * lc),
+                    std::make_pair((void**)&M.ex_rl_t, lc), std::make_pair((void**)&M.ex_sl_s, 4 * nfsp::OBS * sc),
+                    std::make_pair((void**)&M.ex_sl_a, 4 * 3 * sc)}) {
+      NFSP_HIP(hipMalloc(pr.first, (size_t)pr.second));
+      e->allocs.push_back(*pr.first);
+    }
   }
-  if (log_cap) *log_cap = e->M.log_cap;
-  const int64_t so = (int64_t)agent * e->M.sl_cap;
+  const int64_t lo = (int64_t)agent * M.log_cap;
+  const int64_t so = (int64_t)agent * M.sl_cap;
+  if (rl || sl) {
+    const int64_t n = M.log_cap > M.sl_cap ? M.log_cap : M.sl_cap;
+    k_export_mem<<<(unsigned)nfsp_blocks(n, 256), 256, 0, e->ctx->stream>>>(M, agent);
+    NFSP_LAUNCHED("k_export_mem");
+  }
+  if (rl) {
+    rl->s = M.ex_rl_s + lo * nfsp::OBS;
+    rl->a = M.ex_rl_a + lo * 3;
+    rl->r = M.ex_rl_r + lo;
+    rl->s2 = M.ex_rl_s2 + lo * nfsp::OBS;
+    rl->t = M.ex_rl_t + lo;
+    rl->cap = M.log_cap;
+  }
+  if (log_cap) *log_cap = M.log_cap;
   if (sl) {
-    sl->s = e->M.sl_s + so * nfsp::OBS;
-    sl->a = e->M.sl_a + so * 3;
+    sl->s = M.ex_sl_s + so * nfsp::OBS;
+    sl->a = M.ex_sl_a + so * 3;
     sl->r = nullptr;
     sl->s2 = nullptr;
     sl->t = nullptr;

@@ -51,14 +51,32 @@ struct Staging {
   uint4* block_base;   // [nblk]
 };
 
+// On-device record formats.  The reference tuple (utils/replay_buffer.py:
+// 30-41, 53-57: s[30], a[3], r, s2[30], t in fp32 / bool, 257 B) is stored bit-packed: the
+// observations are 0/1 so 30 bits each, r is a multiple of 0.5 in [-13, 13] so an int8 in
+// half units, t a bit; a is kept whole (3 fp32: the stored action vector, net output or
+// uniform draw).  nfsp_engine_memories expands them into the reference's fp32 layout.
+struct __attribute__((aligned(16))) RlRec {     // one M_RL record, 32 B
+  uint32_t s, s2;      // observation bits before / after
+  uint32_t meta;       // argmax(a) | t << 8 | (r in half units, int8) << 16  (= BrRow.meta)
+  float a0, a1, a2;    // the stored action vector
+  uint32_t pad[2];
+};
+struct __attribute__((aligned(16))) SlRec {     // one M_SL record, 16 B (utils/ReservoirBuffer.py)
+  uint32_t x;          // observation bits
+  float a0, a1, a2;    // the behaviour vector (raw Q values or the uniform draw)
+};
+
 struct Memories {
-  // M_RL: circular logs, agent-major [2][log_cap][...] (fp32 reference layout)
-  float *rl_s, *rl_a, *rl_r, *rl_s2;
-  uint8_t* rl_t;
+  // M_RL: circular logs, agent-major [2][log_cap]
+  RlRec* rl;
   int64_t log_cap;
-  // M_SL: reservoirs [2][sl_cap][...]
-  float *sl_s, *sl_a;
+  // M_SL: reservoirs [2][sl_cap]
+  SlRec* sl;
   int64_t sl_cap;
+  // fp32 export views in the reference layout, allocated on first nfsp_engine_memories
+  float *ex_rl_s, *ex_rl_a, *ex_rl_r, *ex_rl_s2, *ex_sl_s, *ex_sl_a;
+  uint8_t* ex_rl_t;
   // pending SL records of the last rollout [2][pend_cap], insert order
   uint32_t* pend_x;
   float* pend_a;

@@ -50,13 +50,6 @@ struct PrepArgs {
   float lr_ar;
 };
 
-__device__ inline uint32_t row_bits(const float* __restrict__ r) {
-  uint32_t b = 0;
-#pragma unroll
-  for (int f = 0; f < nfsp::OBS; ++f) b |= (r[f] != 0.f ? 1u : 0u) << f;
-  return b;
-}
-
 // ---------------------------------------------------------------------------
 // BR prep: rows of update u of agent a (agent/agent.py:217 sample_batch)
 // ---------------------------------------------------------------------------
@@ -76,13 +69,11 @@ __global__ void __launch_bounds__(128) k_br_prep(PrepArgs P) {
   const int64_t slot = (int64_t)a * P.LB.umax + u;
   if (b < P.B) {
     const int64_t row = (int64_t)a * P.M.log_cap + cand[b] % P.M.log_cap;
+    const uint4 q = *reinterpret_cast<const uint4*>(&P.M.rl[row]);   // s, s2, meta, a0
     BrRow rr;
-    rr.s = row_bits(P.M.rl_s + row * nfsp::OBS);
-    rr.s2 = row_bits(P.M.rl_s2 + row * nfsp::OBS);
-    const float* ar = P.M.rl_a + row * 3;
-    const int am = nfsp::argmax3(ar[0], ar[1], ar[2]);
-    const int rh = (int)(P.M.rl_r[row] * 2.0f);
-    rr.meta = (uint32_t)am | ((uint32_t)P.M.rl_t[row] << 8) | (((uint32_t)rh & 0xFFu) << 16);
+    rr.s = q.x;
+    rr.s2 = q.y;
+    rr.meta = q.z;
     P.LB.br_rows[slot * P.B + b] = rr;
   }
   const bool last = u == pl.U_br - 1;
@@ -234,11 +225,11 @@ __global__ void __launch_bounds__(128) k_ar_prep(PrepArgs P) {
       ra[b][1] = P.M.pend_a[qi * 3 + 1];
       ra[b][2] = P.M.pend_a[qi * 3 + 2];
     } else {
-      const int64_t row = (int64_t)a * P.M.sl_cap + j;
-      rx[b] = row_bits(P.M.sl_s + row * nfsp::OBS);
-      ra[b][0] = P.M.sl_a[row * 3 + 0];
-      ra[b][1] = P.M.sl_a[row * 3 + 1];
-      ra[b][2] = P.M.sl_a[row * 3 + 2];
+      const SlRec r = P.M.sl[(int64_t)a * P.M.sl_cap + j];
+      rx[b] = r.x;
+      ra[b][0] = r.a0;
+      ra[b][1] = r.a1;
+      ra[b][2] = r.a2;
     }
   }
   const bool last = u == pl.U - 1;
@@ -267,12 +258,12 @@ __global__ void __launch_bounds__(256) k_res_apply(PrepArgs P) {
   const int64_t slot = P.LB.res_slot[qi];
   if (slot < 0) return;
   if (latest_insert(P.LB, P.M, a, slot, P.A[a].n_sl, P.tag) != q) return;   // a later add wins
-  const uint32_t x = P.M.pend_x[qi];
-  const int64_t row = (int64_t)a * P.M.sl_cap + slot;
-#pragma unroll
-  for (int f = 0; f < nfsp::OBS; ++f) P.M.sl_s[row * nfsp::OBS + f] = (float)((x >> f) & 1u);
-#pragma unroll
-  for (int c = 0; c < 3; ++c) P.M.sl_a[row * 3 + c] = P.M.pend_a[qi * 3 + c];
+  SlRec r;
+  r.x = P.M.pend_x[qi];
+  r.a0 = P.M.pend_a[qi * 3 + 0];
+  r.a1 = P.M.pend_a[qi * 3 + 1];
+  r.a2 = P.M.pend_a[qi * 3 + 2];
+  P.M.sl[(int64_t)a * P.M.sl_cap + slot] = r;
 }
 
 // ---------------------------------------------------------------------------
