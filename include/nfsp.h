@@ -41,6 +41,10 @@ extern "C" {
 #define NFSP_ENOMEM (-3)
 
 #define NFSP_GAME_LEDUC 0
+/* Kuhn swap-in (BASELINE config C5): the same 30-bit observation layout (history bits of
+ * round 0, card one-hot at bit 24 + rank), 3 distinct ranks (0 best), antes 1 / 1, one
+ * betting round with at most one bet (further raises remap to call), showdown by rank. */
+#define NFSP_GAME_KUHN 1
 
 /* MLP output activation / loss (agent/agent.py:103,106,112,115) */
 #define NFSP_ACT_RELU 0        /* BR / target-BR head, Huber loss */

@@ -34,18 +34,21 @@ extern "C" int nfsp_device_count(int* out) {
 // ---------------------------------------------------------------------------
 __global__ void k_env_reset(Hand* __restrict__ hands, int n, const uint8_t* __restrict__ dealer,
                             const uint8_t* __restrict__ ranks, uint32_t k0, uint32_t k1,
-                            uint32_t reset_lo, uint32_t reset_hi) {
+                            uint32_t reset_lo, uint32_t reset_hi, int game) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  uint8_t r0, r1, rp;
+  uint8_t r0, r1, rp = 0;
   if (ranks) {
     r0 = ranks[3 * i]; r1 = ranks[3 * i + 1]; rp = ranks[3 * i + 2];
   } else {
     const nfsp::u32x4 u = nfsp::philox4x32({(uint32_t)i, reset_lo, reset_hi, 0xDEA1u}, k0, k1);
-    nfsp::deal_from_draws(nfsp::below(u.x, 6), nfsp::below(u.y, 5), nfsp::below(u.z, 4), r0, r1, rp);
+    if (game == nfsp::GAME_KUHN)
+      nfsp::deal_kuhn(nfsp::below(u.x, 3), nfsp::below(u.y, 2), r0, r1);
+    else
+      nfsp::deal_from_draws(nfsp::below(u.x, 6), nfsp::below(u.y, 5), nfsp::below(u.z, 4), r0, r1, rp);
   }
   Hand h;
-  nfsp::hand_reset(h, dealer[i] & 1, r0, r1, rp);
+  nfsp::hand_reset(h, dealer[i] & 1, r0, r1, rp, game);
   hands[i] = h;
 }
 
@@ -91,7 +94,7 @@ __global__ void k_env_round(const Hand* __restrict__ hands, int n, uint8_t* __re
 extern "C" int nfsp_create(nfsp_ctx** out, int n_envs, uint64_t seed, int game, int device) {
   NFSP_REQUIRE(out, "out is null");
   NFSP_REQUIRE(n_envs > 0, "n_envs must be > 0");
-  NFSP_REQUIRE(game == NFSP_GAME_LEDUC, "unsupported game");
+  NFSP_REQUIRE(game == NFSP_GAME_LEDUC || game == NFSP_GAME_KUHN, "unsupported game");
   *out = nullptr;
   NFSP_HIP(hipSetDevice(device));
   nfsp_ctx* c = new nfsp_ctx();
@@ -151,7 +154,7 @@ extern "C" int nfsp_env_reset(nfsp_ctx* c, const uint8_t* dealer) {
   const uint64_t ri = c->resets++;
   k_env_reset<<<nfsp_blocks(c->n_envs, 256), 256, 0, c->stream>>>(
       c->hands, c->n_envs, dealer, c->has_pending_deal ? c->pending_deal : nullptr,
-      (uint32_t)c->seed, (uint32_t)(c->seed >> 32), (uint32_t)ri, (uint32_t)(ri >> 32));
+      (uint32_t)c->seed, (uint32_t)(c->seed >> 32), (uint32_t)ri, (uint32_t)(ri >> 32), c->game);
   NFSP_LAUNCHED("k_env_reset");
   c->has_pending_deal = false;
   return NFSP_OK;

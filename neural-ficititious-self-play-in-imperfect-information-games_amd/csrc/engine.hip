@@ -39,6 +39,7 @@ struct RolloutArgs {
   uint32_t g_lo, g_hi;      // hand index of this rollout (per lane)
   float eta;
   unsigned quirks;
+  int game;                 // nfsp::GAME_LEDUC | GAME_KUHN
   const float* w;           // [2][3][NP]
   EngineDev* st;
   Staging S;
@@ -69,10 +70,13 @@ __global__ void __launch_bounds__(256) k_rollout(RolloutArgs A) {
     const double eps0 = A.st->epsilon[0], eps1 = A.st->epsilon[1];
     const int dealer = (int)((L + A.g_lo) & 1u);
     const int lhand = 1 - dealer;
-    uint8_t r0, r1, rp;
+    uint8_t r0, r1, rp = 0;
     {
       const u32x4 u = nfsp::philox4x32({(uint32_t)L, A.g_lo, A.g_hi, 0u}, A.k0, A.k1);
-      nfsp::deal_from_draws(nfsp::below(u.x, 6), nfsp::below(u.y, 5), nfsp::below(u.z, 4), r0, r1, rp);
+      if (A.game == nfsp::GAME_KUHN)
+        nfsp::deal_kuhn(nfsp::below(u.x, 3), nfsp::below(u.y, 2), r0, r1);
+      else
+        nfsp::deal_from_draws(nfsp::below(u.x, 6), nfsp::below(u.y, 5), nfsp::below(u.z, 4), r0, r1, rp);
     }
     // eta draws, dealer first (main.py:36-45): 'a' (AR) iff random() > eta
     int polBR[2];
@@ -82,7 +86,7 @@ __global__ void __launch_bounds__(256) k_rollout(RolloutArgs A) {
       polBR[lhand] = !(nfsp::u01(u.y) > A.eta);
     }
     Hand h;
-    nfsp::hand_reset(h, dealer, r0, r1, rp);
+    nfsp::hand_reset(h, dealer, r0, r1, rp, A.game);
     const bool alias = (A.quirks & NFSP_QUIRK_ALIAS_RL) != 0;
     int nrl = 0, nsl = 0, nrlp[2] = {0, 0}, nslp[2] = {0, 0};
     int dec = 0;
@@ -513,6 +517,7 @@ extern "C" int nfsp_rollout(nfsp_engine* e) {
   A.g_hi = (uint32_t)(e->rollouts >> 32);
   A.eta = e->cfg.eta;
   A.quirks = e->cfg.quirks;
+  A.game = e->ctx->game;
   A.w = e->w;
   A.st = e->st;
   A.S = e->S;

@@ -71,6 +71,14 @@ __host__ __device__ inline void deal_from_draws(uint32_t j5, uint32_t j4, uint32
   rp = d[3] >> 1;
 }
 
+// Kuhn swap-in (BASELINE config C5): a 3-card deck of distinct ranks
+// (0 = best); P0's card = below(3) of the deck, P1's = one of the two left.
+constexpr int GAME_LEDUC = 0, GAME_KUHN = 1;
+__host__ __device__ inline void deal_kuhn(uint32_t j3, uint32_t j2, uint8_t& r0, uint8_t& r1) {
+  r0 = (uint8_t)j3;
+  r1 = (uint8_t)((j3 + 1 + j2) % 3);
+}
+
 // numpy.argmax over 3 floats: the first maximum; a NaN counts as the maximum.
 __host__ __device__ inline int argmax3(float a0, float a1, float a2) {
   if (a0 != a0) return 0;
@@ -96,10 +104,13 @@ struct alignas(16) Hand {
   uint8_t dealer;
   uint8_t rnd, term, raises0, raises1;
   uint8_t slot, ndone, done0, done1;
-  uint8_t done2, c0, c1, pad;   // contributions in half units
+  uint8_t done2, c0, c1, game;  // contributions in half units; GAME_LEDUC | GAME_KUHN
 };
 
-__host__ __device__ inline void hand_reset(Hand& h, int dealer, uint8_t r0, uint8_t r1, uint8_t rp) {
+// Leduc: blinds dealer 0.5 / other 1.0 (leduc/newenv.py:76-114).  Kuhn: antes 1 / 1, one
+// betting round, at most one bet, showdown by rank (no public card).
+__host__ __device__ inline void hand_reset(Hand& h, int dealer, uint8_t r0, uint8_t r1, uint8_t rp,
+                                           int game = GAME_LEDUC) {
   h.hist = 0; h.s[0] = h.s[1] = 0; h.warn = 0;
 #pragma unroll
   for (int i = 0; i < 3; ++i) { h.la[0][i] = 0.f; h.la[1][i] = 0.f; }
@@ -108,9 +119,13 @@ __host__ __device__ inline void hand_reset(Hand& h, int dealer, uint8_t r0, uint
   h.dealer = (uint8_t)dealer;
   h.rnd = 0; h.term = 0; h.raises0 = 0; h.raises1 = 0;
   h.slot = 0; h.ndone = 0; h.done0 = h.done1 = h.done2 = 0;
-  h.c0 = dealer == 0 ? 1 : 2;   // blinds: dealer 0.5, other 1.0
-  h.c1 = dealer == 1 ? 1 : 2;
-  h.pad = 0;
+  h.game = (uint8_t)game;
+  if (game == GAME_KUHN) {
+    h.c0 = h.c1 = 2;              // antes 1.0 each
+  } else {
+    h.c0 = dealer == 0 ? 1 : 2;   // blinds: dealer 0.5, other 1.0
+    h.c1 = dealer == 1 ? 1 : 2;
+  }
 }
 
 // The observation get_state(p) builds (history ++ specific_cards[p]) as 30 bits.
@@ -123,6 +138,14 @@ __host__ __device__ inline uint32_t hand_obs(const Hand& h, int p) {
 __host__ __device__ inline uint8_t& hand_contrib(Hand& h, int p) { return p ? h.c1 : h.c0; }
 __host__ __device__ inline uint8_t& hand_raises(Hand& h, int p) { return p ? h.raises1 : h.raises0; }
 
+// Whether a raise by p is executed as a raise (else do_action remaps it to a call):
+// Leduc leduc/newenv.py:141-145 (p raised this round, or the round so far is [C, R]);
+// Kuhn: one bet per hand.
+__host__ __device__ inline bool hand_raise_legal(const Hand& h, int p) {
+  if (h.game == GAME_KUHN) return h.raises0 + h.raises1 == 0;
+  return !((p ? h.raises1 : h.raises0) > 0 || (h.ndone == 2 && h.done0 == A_CALL && h.done1 == A_RAISE));
+}
+
 // env.step(action, p).  Returns nothing; mirrors every side effect of the reference.
 __host__ __device__ inline void hand_step(Hand& h, int p, float a0, float a1, float a2) {
   h.s[p] = hand_obs(h, p);                      // newenv.py:200-202, even after the end
@@ -131,9 +154,8 @@ __host__ __device__ inline void hand_step(Hand& h, int p, float a0, float a1, fl
   const int raw = argmax3(a0, a1, a2);
   int v = raw;
   h.la[p][0] = a0; h.la[p][1] = a1; h.la[p][2] = a2;
-  if (v == A_RAISE && (hand_raises(h, p) > 0 ||
-                       (h.ndone == 2 && h.done0 == A_CALL && h.done1 == A_RAISE)))
-    v = A_CALL;
+  const bool kuhn = h.game == GAME_KUHN;
+  if (v == A_RAISE && !hand_raise_legal(h, p)) v = A_CALL;
   if (v == A_FOLD) {
     h.term = 1;
   } else {
@@ -149,7 +171,7 @@ __host__ __device__ inline void hand_step(Hand& h, int p, float a0, float a1, fl
       hand_raises(h, p)++;
       c += prev_raise ? 4 : 2;
     }
-    if (opener) c += 1;
+    if (opener && !kuhn) c += 1;                 // the dealer completes its blind
     if (h.ndone == 0) h.done0 = (uint8_t)v;
     else if (h.ndone == 1) h.done1 = (uint8_t)v;
     else h.done2 = (uint8_t)v;
@@ -158,7 +180,7 @@ __host__ __device__ inline void hand_step(Hand& h, int p, float a0, float a1, fl
         (h.ndone == 2 && h.done1 == A_CALL) ||                        // [C,C] [R,C]
         (h.ndone == 3 && h.done1 == A_RAISE && h.done2 == A_CALL);    // [C,R,C] [R,R,C]
     if (over) {
-      if (h.rnd == 1) {
+      if (h.rnd == 1 || kuhn) {
         h.term = 1;
       } else {
         h.rnd = 1;
@@ -175,8 +197,8 @@ __host__ __device__ inline void hand_step(Hand& h, int p, float a0, float a1, fl
       rp_ = -cp; ro_ = cp;
     } else {
       const int kp = h.rank[p], ko = h.rank[o], kb = h.rank[2];
-      if (kp == kb)      { rp_ = co;  ro_ = -cp; }   // pair with the public card
-      else if (ko == kb) { rp_ = -co; ro_ = cp; }
+      if (!kuhn && kp == kb)      { rp_ = co;  ro_ = -cp; }   // pair with the public card
+      else if (!kuhn && ko == kb) { rp_ = -co; ro_ = cp; }    // (Kuhn: no public card)
       else if (kp < ko)  { rp_ = co;  ro_ = -cp; }   // lower rank index wins
       else if (kp > ko)  { rp_ = -co; ro_ = cp; }
       else               { rp_ = 0.f; ro_ = 0.f; }   // draw

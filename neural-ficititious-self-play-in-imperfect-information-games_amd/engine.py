@@ -39,8 +39,9 @@ def glorot_net(rng: np.random.RandomState, hidden: int = 64) -> np.ndarray:
 
 
 class SelfPlayEngine:
-    def __init__(self, ctx: native.Context | None = None, init_seed: int = 0, **cfg):
-        self.ctx = ctx if ctx is not None else native.Context(1)
+    def __init__(self, ctx: native.Context | None = None, init_seed: int = 0, game: int = native.GAME_LEDUC,
+                 **cfg):
+        self.ctx = ctx if ctx is not None else native.Context(1, game=game)
         L = self.ctx.L
         c = native.EngineCfg()
         native.check(L.nfsp_engine_default_cfg(C.byref(c)), "nfsp_engine_default_cfg")

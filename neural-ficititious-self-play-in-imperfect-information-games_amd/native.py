@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("NFSP_LIB", os.path.join(HERE, "libnfsp.so"))
 
 OK, EINVAL, EHIP, ENOMEM = 0, -1, -2, -3
 GAME_LEDUC = 0
+GAME_KUHN = 1     # the Kuhn swap-in (include/nfsp.h NFSP_GAME_KUHN)
 ACT_RELU, ACT_SOFTMAX = 0, 1
 QUIRK_TERMINAL_BOOTSTRAP, QUIRK_ROW0_TARGET, QUIRK_ALIAS_RL = 1, 2, 4
 QUIRKS_REFERENCE = 7
@@ -150,13 +151,13 @@ def stream_handle():
 class Context:
     """Owns one ``nfsp_ctx`` (n envs on the current device), bound to torch's stream."""
 
-    def __init__(self, n_envs: int, seed: int = 1234, device: int | None = None):
+    def __init__(self, n_envs: int, seed: int = 1234, device: int | None = None, game: int = GAME_LEDUC):
         import torch
         L = lib()
         self.L = L
         dev = torch.cuda.current_device() if device is None else device
         h = P()
-        check(L.nfsp_create(C.byref(h), int(n_envs), int(seed) & (2**64 - 1), GAME_LEDUC, dev),
+        check(L.nfsp_create(C.byref(h), int(n_envs), int(seed) & (2**64 - 1), int(game), dev),
               "nfsp_create")
         self.h = h
         self.n = int(n_envs)

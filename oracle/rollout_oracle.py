@@ -87,10 +87,11 @@ def orc_bits(x) -> int:
     return int(sum(int(v[i] != 0) << i for i in range(30)))
 
 
-def rollout_with_positions(n_lanes, g, seed, w_flat, eps, eta=0.1, alias=True, rl_before=(0, 0)):
+def rollout_with_positions(n_lanes, g, seed, w_flat, eps, eta=0.1, alias=True, rl_before=(0, 0),
+                           game="leduc"):
     """rollout() plus, for each SL record, its global RL stream position (what the engine
     stores in its pending list)."""
-    out = rollout_lanes(n_lanes, g, seed, w_flat, eps, eta, alias)
+    out = rollout_lanes(n_lanes, g, seed, w_flat, eps, eta, alias, game)
     rl = ([], [])
     sl = ([], [])
     base = list(rl_before)
@@ -103,13 +104,13 @@ def rollout_with_positions(n_lanes, g, seed, w_flat, eps, eta=0.1, alias=True, r
     return dict(rl=rl, sl=sl, actions=out["actions"], reward=out["reward"])
 
 
-def rollout_lanes(n_lanes, g, seed, w_flat, eps, eta=0.1, alias=True):
+def rollout_lanes(n_lanes, g, seed, w_flat, eps, eta=0.1, alias=True, game="leduc"):
     """Like rollout() but keeps the records per lane."""
     lanes = []
     actions = np.zeros((2, 3), np.int64)
     reward = np.zeros(2)
     for L in range(n_lanes):
-        res = _one_lane(L, g, seed, w_flat, eps, eta, alias)
+        res = _one_lane(L, g, seed, w_flat, eps, eta, alias, game)
         lanes.append(res)
         actions += res["actions"]
         reward += res["reward"]
@@ -119,7 +120,12 @@ def rollout_lanes(n_lanes, g, seed, w_flat, eps, eta=0.1, alias=True):
 _NETS_CACHE = {}
 
 
-def _one_lane(L, g, seed, w_flat, eps, eta, alias):
+def deal_kuhn(j3, j2):
+    """nfsp_device.h deal_kuhn: P0 = below(3), P1 = one of the two ranks left."""
+    return int(j3), int((j3 + 1 + j2) % 3), 0
+
+
+def _one_lane(L, g, seed, w_flat, eps, eta, alias, game="leduc"):
     key = id(w_flat)
     if key not in _NETS_CACHE:
         _NETS_CACHE.clear()
@@ -132,11 +138,14 @@ def _one_lane(L, g, seed, w_flat, eps, eta, alias):
     ex, ey, _, _ = (v[0] for v in philox4x32(one(L), one(glo), one(ghi), one(1), k0, k1))
     dealer = (L + g) & 1
     lhand = 1 - dealer
-    ranks = deal_from_draws(below(dx, 6), below(dy, 5), below(dz, 4))
+    if game == "kuhn":
+        ranks = deal_kuhn(below(dx, 3), below(dy, 2))
+    else:
+        ranks = deal_from_draws(below(dx, 6), below(dy, 5), below(dz, 4))
     pol_br = [False, False]
     pol_br[dealer] = not (u01(ex) > eta)
     pol_br[lhand] = not (u01(ey) > eta)
-    env = orc.Env(deal_source=lambda: ranks)
+    env = orc.Env(deal_source=lambda: ranks, game=game)
     env.reset(dealer)
     hand_rl = []
     n_rl_p = [0, 0]

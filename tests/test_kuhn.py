@@ -1,0 +1,179 @@
+"""Kuhn swap-in (BASELINE config C5).
+
+The reference has no Kuhn game; the swap-in reuses the Leduc machinery (include/nfsp.h
+NFSP_GAME_KUHN).  Its parity is therefore anchored analytically: the oracle evaluator
+scores Kuhn's known Nash equilibrium family (Kuhn 1950; first actor bets the best card with
+3 alpha, bluffs the worst with alpha, calls with the middle card at alpha + 1/3) at
+exploitability 0 and the first actor's value at -1/18, for every alpha in [0, 1/3].  The GPU
+env, evaluator and engine rollout are then checked against the oracle restatement.
+"""
+import itertools
+
+import numpy as np
+import pytest
+
+import exploit_oracle as eo
+import nfsp_oracle as orc
+import nn_oracle as nn
+
+K, Q, J = 0, 1, 2            # rank 0 is the best card
+
+
+def nash(seat, alpha):
+    """Kuhn's equilibrium for `seat`, as a function of its observation bits (history bits
+    12p + 2 slot + act of round 0, card bit 24 + rank)."""
+    o = 1 - seat
+
+    def fn(obs):
+        card = next(r for r in range(3) if (obs >> (24 + r)) & 1)
+        h = obs & 0xFFFFFF
+        if h == 0:                                        # first to act
+            b = {K: 3 * alpha, Q: 0.0, J: alpha}[card]
+            return (0.0, 1.0 - b, b)
+        if h == 1 << (12 * o):                            # second, facing a check
+            b = {K: 1.0, Q: 0.0, J: 1.0 / 3.0}[card]
+            return (0.0, 1.0 - b, b)
+        if h == 1 << (12 * o + 1):                        # second, facing a bet
+            c = {K: 1.0, Q: 1.0 / 3.0, J: 0.0}[card]
+            return (1.0 - c, c, 0.0)
+        if h == (1 << (12 * seat)) | (1 << (12 * o + 3)):  # first, checked, facing a bet
+            c = {K: 1.0, Q: alpha + 1.0 / 3.0, J: 0.0}[card]
+            return (1.0 - c, c, 0.0)
+        raise AssertionError(f"unreachable Kuhn observation {h:#x}")
+    return eo.TabularPolicy(fn)
+
+
+@pytest.mark.parametrize("alpha", [0.0, 0.1, 1.0 / 3.0])
+def test_oracle_kuhn_nash_is_unexploitable(alpha):
+    p0, p1 = nash(0, alpha), nash(1, alpha)
+    r = eo.exploitability_of(p0, p1, "kuhn")
+    assert abs(r["exploitability"]) < 1e-12
+    assert abs(r["value0"]) < 1e-12                       # dealer alternation: seats equal
+    # seat 0 always first to act: the game value -1/18
+    v = eo.on_policy_value0(p0, p1, "kuhn", dealers=(0,))
+    assert v == pytest.approx(-1.0 / 18.0, abs=1e-12)
+
+
+def test_oracle_kuhn_deviation_is_exploitable():
+    p0, p1 = nash(0, 0.1), nash(1, 0.1)
+    always_bet = eo.TabularPolicy(lambda obs: (0.0, 0.0, 1.0))
+    assert eo.exploitability_of(always_bet, p1, "kuhn")["exploitability"] > 0.05
+    assert eo.exploitability_of(p0, always_bet, "kuhn")["exploitability"] > 0.05
+
+
+def test_oracle_kuhn_env_rules():
+    env = orc.Env(deal_source=lambda: (K, J, 0), game="kuhn")
+    env.reset(0)
+    assert env.contrib == [2, 2]                         # antes 1 / 1
+    env.step(np.array([0, 0, 1.0]), 0)                   # bet
+    env.step(np.array([0, 0, 1.0]), 1)                   # a re-raise is remapped to a call
+    assert env.terminated and env.reward[0] == 2.0 and env.reward[1] == -2.0
+    env.reset(1)
+    env.step(np.array([0, 1.0, 0]), 1)                   # check
+    env.step(np.array([0, 1.0, 0]), 0)                   # check: showdown, K beats J
+    assert env.terminated and env.reward[0] == 1.0
+    env.reset(0)
+    env.step(np.array([1.0, 0, 0]), 0)                   # fold: loses the ante
+    assert env.terminated and env.reward[0] == -1.0 and env.reward[1] == 1.0
+
+
+# ---- GPU ----------------------------------------------------------------------
+@pytest.mark.gpu
+def test_gpu_kuhn_env_exhaustive(pkg):
+    """Every deal x dealer x raw action sequence (fold/call/raise, 4 deep; the actor
+    alternates from the dealer, steps after the end included) through the batched env
+    (nfsp_env_*, one env per case) vs the oracle Env: both players' get_state after every
+    step, bit for bit."""
+    import torch
+    nat = pkg.native
+    cases = [(r0, r1, d, seq) for r0, r1 in itertools.permutations(range(3), 2) for d in (0, 1)
+             for seq in itertools.product(range(3), repeat=4)]
+    n = len(cases)
+    ctx = nat.Context(n, seed=3, game=nat.GAME_KUHN)
+    dev = "cuda"
+    ranks = torch.tensor([[c[0], c[1], 0] for c in cases], dtype=torch.uint8, device=dev)
+    dealer = torch.tensor([c[2] for c in cases], dtype=torch.uint8, device=dev)
+    ctx.call("nfsp_env_set_deal", nat.ptr(ranks))
+    ctx.call("nfsp_env_reset", nat.ptr(dealer))
+    envs = []
+    for (r0, r1, d, _) in cases:
+        e = orc.Env(deal_source=lambda r0=r0, r1=r1: (r0, r1, 0), game="kuhn")
+        e.reset(d)
+        envs.append(e)
+    s = torch.empty((n, 30), device=dev)
+    a = torch.empty((n, 3), device=dev)
+    r = torch.empty(n, device=dev)
+    s2 = torch.empty((n, 30), device=dev)
+    t = torch.empty(n, dtype=torch.uint8, device=dev)
+    w = (1 << np.arange(30, dtype=np.int64))
+    for k in range(5):
+        if k > 0:
+            pl = np.array([(c[2] + k - 1) % 2 for c in cases], np.uint8)
+            act = np.zeros((n, 3), np.float32)
+            act[np.arange(n), [c[3][k - 1] for c in cases]] = 1.0
+            # keep the device buffers referenced until the stream has consumed them
+            act_d = torch.as_tensor(act, device=dev)
+            pl_d = torch.as_tensor(pl, device=dev)
+            mask_d = torch.ones(n, dtype=torch.uint8, device=dev)
+            ctx.call("nfsp_env_step", nat.ptr(act_d), 0, nat.ptr(pl_d), nat.ptr(mask_d))
+            torch.cuda.synchronize()
+            for i, e in enumerate(envs):
+                e.step(act[i].astype(np.float64), int(pl[i]))
+        for p in (0, 1):
+            ctx.call("nfsp_env_get_state", p, None, nat.ptr(s), nat.ptr(a), nat.ptr(r), nat.ptr(s2), nat.ptr(t))
+            sb = (s.cpu().numpy().astype(np.int64) * w).sum(axis=1)
+            s2b = (s2.cpu().numpy().astype(np.int64) * w).sum(axis=1)
+            for i, e in enumerate(envs):
+                es, ea, er, es2, et = e.get_state(p)
+                assert sb[i] == orc_bits(es) and s2b[i] == orc_bits(es2), (k, p, cases[i])
+                assert np.array_equal(a[i].cpu().numpy().astype(np.float64), ea.reshape(3)), (k, p, cases[i])
+                assert float(r[i]) == float(er) and bool(t[i]) == bool(et), (k, p, cases[i])
+
+
+def orc_bits(x):
+    v = np.asarray(x).reshape(-1)
+    return int(sum(int(v[i] != 0) << i for i in range(30)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1])
+def test_gpu_kuhn_exploitability_matches_oracle(pkg, mode):
+    import torch
+    rng = np.random.RandomState(5)
+    w0 = nn.MLP(nn.ACT_SOFTMAX, 64, rng=rng).flat()
+    w1 = nn.MLP(nn.ACT_SOFTMAX, 64, rng=rng).flat()
+    ctx = pkg.native.Context(1, game=pkg.native.GAME_KUHN)
+    d0, d1 = torch.as_tensor(w0, device="cuda"), torch.as_tensor(w1, device="cuda")
+    got = pkg.engine.exploitability(ctx, d0.data_ptr(), d1.data_ptr(), mode)
+    want = eo.exploitability(w0, w1, mode, "kuhn")
+    for k in ("br0", "br1", "exploitability", "value0"):
+        assert got[k] == pytest.approx(want[k], abs=1e-5), k
+
+
+@pytest.mark.gpu
+def test_gpu_kuhn_engine_rollout_matches_oracle(pkg):
+    """The fused rollout with game = Kuhn against rollout_oracle's Kuhn lanes."""
+    import rollout_oracle as R
+    from test_gpu_engine import check_rollout, weights_flat
+    N, seed = 2000, 99
+    eng = pkg.engine.SelfPlayEngine(n_lanes=N, seed=seed, init_seed=4, eta=0.3, inserts_per_update=1 << 30,
+                                    game=pkg.native.GAME_KUHN)
+    w = weights_flat(eng)
+    eng.rollout()
+    ref = R.rollout_with_positions(N, 0, seed, w, (0.06, 0.06), eta=0.3, alias=True, game="kuhn")
+    check_rollout(eng, ref)
+    st = eng.stats()
+    assert np.array_equal(np.array(st["actions"]), ref["actions"])
+    assert np.allclose(st["reward"], ref["reward"])
+
+
+@pytest.mark.gpu
+def test_gpu_kuhn_training_lowers_exploitability(pkg):
+    """C5's correctness direction: self-play on Kuhn moves the AR nets toward equilibrium."""
+    eng = pkg.engine.SelfPlayEngine(n_lanes=8192, rl_capacity=40_000, sl_capacity=40_000, seed=21,
+                                    game=pkg.native.GAME_KUHN)
+    e0 = eng.exploitability(0)["exploitability"]
+    for _ in range(60):
+        eng.step()
+    e1 = eng.exploitability(0)["exploitability"]
+    assert e1 < e0
