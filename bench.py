@@ -103,7 +103,7 @@ def init_dist(backend=None):
     import torch.distributed as dist
     backend = backend or "nccl"
     if backend == "nccl":
-        dist.init_process_group(backend, device_id=torch.device("cuda", local))
+        dist.init_process_group(backend, device_id=torch.device("cuda", local % torch.cuda.device_count()))
     else:
         dist.init_process_group(backend)
     return world, rank, local, dist
@@ -146,12 +146,14 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL (one rank per GPU); gloo: a CPU-side rehearsal of the N > 1 path")
     args = ap.parse_args()
 
     import torch
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    world, rank, local, dist = init_dist()
+    torch.cuda.set_device(local % torch.cuda.device_count())   # one rank per GPU (mod: rehearsals)
+    world, rank, local, dist = init_dist(args.dist_backend)
 
     import __graft_entry__
     pkg = __graft_entry__.load_package()
@@ -165,7 +167,8 @@ def main():
     s0 = eng.stats()
     eng.set_timing(True)
     eng.timings()
-    elapsed = timed_steps(eng.step, args.steps, 0, dist, torch.cuda.synchronize)
+    elapsed = timed_steps(eng.step, args.steps, 0, dist, torch.cuda.synchronize,
+                          device="cuda" if args.dist_backend == "nccl" else "cpu")
     timings = eng.timings()
     s1 = eng.stats()
 
