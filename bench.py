@@ -18,14 +18,20 @@ scaling); a barrier and a max-over-ranks of the elapsed time bracket the timed r
 
 Roofline: HIP events recorded on the engine's stream around every kernel launch give
 each kernel's average duration; the dominant kernel's algorithmic FLOPs (or bytes) per
-launch / that duration is `roofline.achieved`.  `cpu_baseline`: the oracle restatement
-of the reference's main.train (oracle/nfsp_oracle.py, reference cadence, numpy MLPs) on
-one host core for a bounded number of seconds.
+launch / that duration is `roofline.achieved`.
+
+`cpu_baseline` (rank 0, N = 1 only) comes from the C++ restatement of the reference's
+main.train (oracle/nfsp_cpu.cpp).  It uses the reference cadence and this config's memory
+capacities, and is parity-checked hand for hand against oracle/nfsp_oracle.py.  It runs as
+one independent replica per host thread (`--cpu-threads`, default 16: the box's CPU share)
+for `--cpu-seconds`; `per_core` is one replica alone.  `cpu_baseline_numpy` is the numpy
+restatement on one core for 5 s.
 """
 from __future__ import annotations
 
 import argparse
 import json
+import subprocess
 import os
 import sys
 import time
@@ -68,8 +74,8 @@ def load_pmc(config, kernel):
     return None if k is None else k.get("hbm_bytes_per_launch")
 
 
-def cpu_baseline(seconds: float):
-    """The reference-structured CPU path: oracle Env/Agent + main.train's loop."""
+def cpu_baseline_numpy(seconds: float):
+    """The reference-structured CPU path in numpy: oracle Env/Agent + main.train's loop."""
     import random
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import nfsp_oracle as orc
@@ -86,9 +92,30 @@ def cpu_baseline(seconds: float):
             hands += 1
     dt = time.perf_counter() - t0
     return {"value": hands / dt, "unit": "hands/s", "cores": 1, "kind": "port",
-            "sample": f"{hands} hands of main.train restated on the CPU (oracle/nfsp_oracle.py: "
+            "sample": f"{hands} hands of main.train restated in numpy (oracle/nfsp_oracle.py: "
                       f"Env, Agent play/updates at the reference cadence, numpy fp32 MLPs), "
                       f"{dt:.1f} s on one core"}
+
+
+def cpu_baseline(seconds: float, threads: int, cfg: dict):
+    """main.train restated in C++ (oracle/nfsp_cpu.cpp, parity-checked hand for hand against
+    oracle/nfsp_oracle.py by tests/test_cpu_port.py), one independent replica per host
+    thread at this config's memory capacities.  Host threads: the box's CPU share."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import cpu_port
+    if not os.path.exists(cpu_port.LIB_PATH):
+        subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle")], check=True)
+    c = cpu_port.make_cfg(None, 0, True, "leduc", rl_capacity=cfg["rl_capacity"],
+                          sl_capacity=cfg["sl_capacity"])
+    one, el1 = cpu_port.bench(c, 1, min(seconds, 5.0))
+    hands, el = cpu_port.bench(c, threads, seconds)
+    return {"value": hands / el, "unit": "hands/s", "cores": threads, "kind": "port",
+            "per_core": one / el1,
+            "sample": f"{hands} hands of main.train restated in C++ (oracle/nfsp_cpu.cpp: the "
+                      f"reference's Env, scheduler, memories M_RL {cfg['rl_capacity']:,} / M_SL "
+                      f"{cfg['sl_capacity']:,}, updates at the reference cadence, fp32 MLPs) by "
+                      f"{threads} independent replicas (one learner each) in {el:.1f} s; one "
+                      f"replica alone: {one / el1:,.0f} hands/s"}
 
 
 def init_dist(backend=None):
@@ -144,7 +171,9 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-threads", type=int, default=16,
+                    help="host threads for cpu_baseline (16 = the 1-GPU box's CPU share)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL (one rank per GPU); gloo: a CPU-side rehearsal of the N > 1 path")
@@ -237,8 +266,10 @@ def main():
     out["exploitability_exact"] = {
         "softmax_mixed": ex[0]["exploitability"], "argmax_as_executed": ex[1]["exploitability"],
         "hands_trained_per_gpu": int(s1["hands"]), "unit": "chips (BR_0 + BR_1)"}
-    if rank == 0 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    if rank == 0 and world == 1 and not args.no_cpu:
+        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, threads, cfg)
+        out["cpu_baseline_numpy"] = cpu_baseline_numpy(min(args.cpu_seconds, 5.0))
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
