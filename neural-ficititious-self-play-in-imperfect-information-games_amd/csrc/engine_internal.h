@@ -94,6 +94,10 @@ struct Memories {
 //   ba[g][i]  the same bits of input i's 32-bit mask over the minibatch's 32 samples (the
 //             bit-transposed minibatch: the dW1 = X^T dZ1 operand)
 //   tg[s]     sample s's three fit targets and the step's learning rate
+// Input 30 (CHAIN_BIAS_BIT) is the constant 1 of every sample: the chain keeps b1 as W1's
+// row 30, so the layer-1 products include the bias and dW1's row 30 is gb1.
+constexpr uint32_t CHAIN_BIAS_BIT = 1u << 30;
+constexpr int CHAIN_BIAS_IN = 30;
 struct __attribute__((aligned(16))) StepRec {
   uint4 fa[4][32];
   uint4 ba[4][32];

@@ -127,13 +127,15 @@ __device__ inline uint4 bits8u(uint32_t x, int g) {
 }
 
 // The chain records of one (update, epoch): thread b holds fit position b's observation
-// mask x (0 for b >= B), targets and the lr; minibatch b >> 5 gets fa / tg of its sample
-// b & 31, and ba from the bit transpose of its 32 masks by wave ballot.  Whole block (a
-// multiple of 64 threads) calls.
+// mask x (for b < B), targets and the lr; minibatch b >> 5 gets fa / tg of its sample
+// b & 31, and ba from the bit transpose of its 32 masks by wave ballot.  Every valid
+// sample also carries the bias input (CHAIN_BIAS_BIT).  Whole block (a multiple of 64
+// threads) calls.
 __device__ inline void emit_recs(StepRec* __restrict__ recs, uint32_t x, float t0, float t1, float t2,
                                  float lr, int B) {
   const int b = threadIdx.x;
   if (b < B) {
+    x |= CHAIN_BIAS_BIT;
     StepRec& R = recs[b >> 5];
     const int k = b & 31;
 #pragma unroll
@@ -143,7 +145,7 @@ __device__ inline void emit_recs(StepRec* __restrict__ recs, uint32_t x, float t
   const int lane = b & 63;
   unsigned long long mine = 0;
 #pragma unroll
-  for (int i = 0; i < nfsp::OBS; ++i) {
+  for (int i = 0; i <= CHAIN_BIAS_IN; ++i) {
     const unsigned long long m = __ballot((x >> i) & 1u);
     if (lane == i) mine = m;
   }
@@ -439,11 +441,17 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 __device__ unsigned long long g_chain_stamps[4][4][10];
 #endif
 
+// Stores are unconditional: lanes whose copy is redundant (the odd lane rows of po / dm, the
+// rows g > 0 of w2t, the lanes past a record quarter) write to sink rows nobody reads, so
+// the loop has no exec-mask branches.
 struct Chain3Smem {
-  float po[2][4][32][4];     // per-wave partial layer-2 outputs, double-buffered by step parity
-  float dm[4][3][32];        // wave-private: dL/dz2 of the 32 samples, by output
-  float4 w2t[4][16];         // wave-private: (W2[h][0..2], b1[h]) of the slice, for Z1^T
+  float po[2][4][64][4];     // per-wave partial layer-2 outputs by sample (rows 32..63: sink),
+                             // double-buffered by step parity
+  float dm[4][3][64];        // wave-private: dL/dz2 of the 32 samples, by output (32..63: sink)
+  float4 w2t[4][64];         // wave-private: W2[h][0..2] of the slice for Z1^T (lane l writes
+                             // row l; rows 0..15 are read)
   StepRec ring[4];           // step records t .. t + 2 (slot t & 3), a quarter per wave
+  uint4 rec_sink[64];
 };
 constexpr int REC_CHUNKS = (int)(sizeof(StepRec) / 16);    // 288 x 16 B
 constexpr int REC_QUARTER = REC_CHUNKS / 4;                 // 72 per wave
@@ -497,9 +505,8 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int i = 16 * (j >> 2) + 4 * g + (j & 3);
-    wr[j] = i < nfsp::OBS ? gw[nn::OW1 + i * nn::H + hid] : 0.f;
+    wr[j] = i < nfsp::OBS ? gw[nn::OW1 + i * nn::H + hid] : i == CHAIN_BIAS_IN ? gw[nn::OB1 + hid] : 0.f;
   }
-  float b1 = gw[nn::OB1 + hid];
   float W2_0 = gw[nn::OW2 + 3 * hid + 0], W2_1 = gw[nn::OW2 + 3 * hid + 1], W2_2 = gw[nn::OW2 + 3 * hid + 2];
   float b2_0 = gw[nn::OB2 + 0], b2_1 = gw[nn::OB2 + 1], b2_2 = gw[nn::OB2 + 2];
   const int nmb = C.B / CHAIN_MB;
@@ -521,20 +528,24 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
   const int T1 = (int)(u1 * spu);
   int t = (int)(u0 * spu);
   const uint4* recb = reinterpret_cast<const uint4*>(C.rec + slot0 * spu);
-  // this wave's quarter of record p (clamped), into two registers / back into ring slot p & 3
+  // this wave's quarter of record p (clamped), into two registers / back into ring slot p & 3;
+  // the lanes past the quarter load a duplicate chunk and store it to the sink
+  const bool in_q = l < REC_QUARTER - 64;
+  const int lb = in_q ? 64 + l : REC_QUARTER - 1;
   auto issue = [&](int p, uint4& va, uint4& vb) {
     const uint4* src = recb + (size_t)(p < T1 ? p : T1 - 1) * REC_CHUNKS + REC_QUARTER * w;
     va = src[l];
-    vb = l < REC_QUARTER - 64 ? src[64 + l] : make_uint4(0, 0, 0, 0);
+    vb = src[lb];
   };
   auto stash = [&](int p, const uint4& va, const uint4& vb) {
     uint4* dst = reinterpret_cast<uint4*>(&sm.ring[p & 3]) + REC_QUARTER * w;
     dst[l] = va;
-    if (l < REC_QUARTER - 64) dst[64 + l] = vb;
+    *(in_q ? dst + 64 + l : &sm.rec_sink[l]) = vb;
   };
-  auto publish = [&]() {   // this wave's (W2, b1) rows for its own Z1^T layer 2
-    if (g == 0) sm.w2t[w][c] = make_float4(W2_0, W2_1, W2_2, b1);
+  auto publish = [&]() {   // this wave's W2 rows for its own Z1^T layer 2
+    sm.w2t[w][l] = make_float4(W2_0, W2_1, W2_2, 0.f);
   };
+  const int prow = 32 * (g & 1) + sl;          // po / dm row: the sample, or the sink
 #ifdef NFSP_CHAIN_STAMPS
   unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_last = 0;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
@@ -556,11 +567,11 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
     // ---- layer 1, both orientations
     bf16x8 whi, wmid, wlo;
     split3(wr, whi, wmid, wlo);
-    float W2h[4][3], b1h[4];
+    float W2h[4][3];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float4 q = sm.w2t[w][4 * g + r];
-      W2h[r][0] = q.x; W2h[r][1] = q.y; W2h[r][2] = q.z; b1h[r] = q.w;
+      W2h[r][0] = q.x; W2h[r][1] = q.y; W2h[r][2] = q.z;
     }
     // Z1^T first (layer 2 waits on it); Z1 (needed only by the backward) is issued after
     // layer 2, so its matrix-core time overlaps the barrier wait
@@ -574,8 +585,8 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
     for (int k = 0; k < 3; ++k) { p0[k] = 0.f; p1[k] = 0.f; }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float h0 = fmaxf(zh0[r] + b1h[r], 0.f);
-      const float h1 = fmaxf(zh1[r] + b1h[r], 0.f);
+      const float h0 = fmaxf(zh0[r], 0.f);        // b1 is W1's row 30 (CHAIN_BIAS_IN)
+      const float h1 = fmaxf(zh1[r], 0.f);
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
         p0[k] = p0[k] + h0 * W2h[r][k];
@@ -590,7 +601,7 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
       q[k] = sum_x16(__uint_as_float(rr[0]) + __uint_as_float(rr[1]));
     }
     const int buf = t & 1;
-    if ((g & 1) == 0) *reinterpret_cast<float4*>(&sm.po[buf][w][sl][0]) = make_float4(q[0], q[1], q[2], 0.f);
+    *reinterpret_cast<float4*>(&sm.po[buf][w][prow][0]) = make_float4(q[0], q[1], q[2], 0.f);
     __builtin_amdgcn_sched_barrier(0);
     const floatx4 zs0 = mfma3(fa0, whi, wmid, wlo);      // Z1: sample 4g+r, hidden 16w+c
     const floatx4 zs1 = mfma3(fa1, whi, wmid, wlo);      //     sample 16+4g+r
@@ -619,10 +630,10 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
         float dd[3];
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-          const float y = oz[k] > 0.f ? oz[k] : 0.f;
-          const float ee = tt[k] - y;
-          const float gg = fabsf(ee) > 1.0f ? (ee > 0.f ? 1.f : -1.f) : ee;
-          dd[k] = oz[k] > 0.f ? (-gg * inv3m) : 0.f;
+          const float ee = tt[k] - fmaxf(oz[k], 0.f);
+          // |e| > 1 ? sign(e) : e  ==  clamp(e, -1, 1)
+          const float gg = __builtin_amdgcn_fmed3f(ee, -1.f, 1.f);
+          dd[k] = oz[k] > 0.f ? gg * -inv3m : 0.f;
         }
         d0 = dd[0]; d1 = dd[1]; d2 = dd[2];
       } else {
@@ -680,11 +691,9 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
         }
       }
     }
-    if ((g & 1) == 0) {
-      sm.dm[w][0][sl] = d0;
-      sm.dm[w][1][sl] = d1;
-      sm.dm[w][2][sl] = d2;
-    }
+    sm.dm[w][0][prow] = d0;
+    sm.dm[w][1][prow] = d1;
+    sm.dm[w][2][prow] = d2;
     float gb2[3] = {d0, d1, d2};     // sum over the 32 samples: the row's 16, then rows g ^ 2
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -704,38 +713,35 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
       dB[k] = *reinterpret_cast<const float4*>(&sm.dm[w][k][16 + 4 * g]);
     }
     float dz[8];
-    float g2_0 = 0.f, g2_1 = 0.f, g2_2 = 0.f, gb1 = 0.f;
+    float g2_0 = 0.f, g2_1 = 0.f, g2_2 = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int r = j & 3;
-      const float z = (j < 4 ? zs0[r] : zs1[r]) + b1;
+      const float z = j < 4 ? zs0[r] : zs1[r];
       const float4 e0 = j < 4 ? dA[0] : dB[0], e1 = j < 4 ? dA[1] : dB[1], e2 = j < 4 ? dA[2] : dB[2];
       const float x0 = r == 0 ? e0.x : r == 1 ? e0.y : r == 2 ? e0.z : e0.w;
       const float x1 = r == 0 ? e1.x : r == 1 ? e1.y : r == 2 ? e1.z : e1.w;
       const float x2 = r == 0 ? e2.x : r == 1 ? e2.y : r == 2 ? e2.z : e2.w;
-      const float h = z > 0.f ? z : 0.f;
+      const float h = fmaxf(z, 0.f);
       g2_0 += h * x0;
       g2_1 += h * x1;
       g2_2 += h * x2;
       const float dh = (x0 * W2_0 + x1 * W2_1) + x2 * W2_2;
       dz[j] = z > 0.f ? dh : 0.f;
-      gb1 += dz[j];
     }
     bf16x8 dhi, dmid, dlo;
     split3(dz, dhi, dmid, dlo);
-    // dW1[16 it + 4g + r][16w + c] = sum over the 32 samples in dz's K order
+    // dW1[16 it + 4g + r][16w + c] = sum over the 32 samples in dz's K order (row 30: gb1)
     const floatx4 gA = mfma3(ba0, dhi, dmid, dlo);
     const floatx4 gB = mfma3(ba1, dhi, dmid, dlo);
     g2_0 = sum_x16(sum_x32(g2_0));
     g2_1 = sum_x16(sum_x32(g2_1));
     g2_2 = sum_x16(sum_x32(g2_2));
-    gb1 = sum_x16(sum_x32(gb1));
     CHAIN_STAMP(4);
     const float lr = lr_step;
     W2_0 = W2_0 - lr * g2_0;
     W2_1 = W2_1 - lr * g2_1;
     W2_2 = W2_2 - lr * g2_2;
-    b1 = b1 - lr * gb1;
     b2_0 = b2_0 - lr * gb2[0];
     b2_1 = b2_1 - lr * gb2[1];
     b2_2 = b2_2 - lr * gb2[2];
@@ -784,9 +790,9 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
     for (int j = 0; j < 8; ++j) {
       const int i = 16 * (j >> 2) + 4 * g + (j & 3);
       if (i < nfsp::OBS) dst[nn::OW1 + i * nn::H + hid] = wr[j];
+      else if (i == CHAIN_BIAS_IN) dst[nn::OB1 + hid] = wr[j];
     }
     if (g == 0) {
-      dst[nn::OB1 + hid] = b1;
       dst[nn::OW2 + 3 * hid + 0] = W2_0;
       dst[nn::OW2 + 3 * hid + 1] = W2_1;
       dst[nn::OW2 + 3 * hid + 2] = W2_2;

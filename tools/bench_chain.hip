@@ -2,7 +2,8 @@
 // records: microseconds per SGD step, and with -DNFSP_CHAIN_STAMPS the per-phase cycle
 // split of waves 0..3 (s_memtime).  Mode "compare" checks k_chain3 against the previous
 // f32-MFMA chain (tools/chain_ref.hip) from the same start.  Not part of libnfsp.
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude -I<pkg>/csrc tools/bench_chain.hip
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -mllvm -amdgpu-mfma-vgpr-form -fno-slp-vectorize \
+//         -Iinclude -I<pkg>/csrc tools/bench_chain.hip   (the flags of learner.hip in build())
 //   ./bench_chain <updates> <relu 0|1> [time|compare] [blocks 1|2] [layer-2 weight scale]
 #include <math.h>
 #include <stdio.h>
@@ -62,9 +63,10 @@ int main(int argc, char** argv) {
     uint32_t xt[32] = {0};
     for (int k = 0; k < 32; ++k) {
       const auto& r = fit[st * 32 + k];
-      for (int g = 0; g < 4; ++g) rec[st].fa[g][k] = bits8_host(r.x, g);
+      const uint32_t xb = r.x | CHAIN_BIAS_BIT;      // emit_recs: the bias input
+      for (int g = 0; g < 4; ++g) rec[st].fa[g][k] = bits8_host(xb, g);
       rec[st].tg[k] = make_float4(r.t0, r.t1, r.t2, lr);
-      for (int i = 0; i < 30; ++i) if ((r.x >> i) & 1u) xt[i] |= 1u << k;
+      for (int i = 0; i <= CHAIN_BIAS_IN; ++i) if ((xb >> i) & 1u) xt[i] |= 1u << k;
     }
     for (int i = 0; i < 32; ++i)
       for (int g = 0; g < 4; ++g) rec[st].ba[g][i] = bits8_host(xt[i], g);
