@@ -461,19 +461,31 @@ static_assert(REC_CHUNKS % 4 == 0 && REC_QUARTER > 64 && REC_QUARTER <= 128, "re
 constexpr int CHAIN_LDS = 150 * 1024;
 static_assert(sizeof(Chain3Smem) <= CHAIN_LDS, "chain LDS");
 
-// exact three-term bf16 split of 8 f32 values
+// exact three-term bf16 split of 8 f32 values, a pair at a time: one packed conversion
+// per pair and level (v_cvt_pk_bf16_f32, round to nearest even), the two f32 values of the
+// packed pair by shift / mask, and the two residuals.  v = hi + mid + lo exactly.
+// (inline asm: as plain conversions the compiler re-derives the low half by a second
+// single-value conversion instead of shifting the packed word)
+__device__ inline uint32_t cvt_pk_bf16(float a, float b) {
+  uint32_t r;
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 __device__ inline void split3(const float (&v)[8], bf16x8& hi, bf16x8& mid, bf16x8& lo) {
 #pragma clang fp contract(off)
+  uint32_t h[4], m[4], o[4];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const __bf16 h = (__bf16)v[j];
-    const float r1 = v[j] - (float)h;
-    const __bf16 m = (__bf16)r1;
-    const float r2 = r1 - (float)m;
-    hi[j] = h;
-    mid[j] = m;
-    lo[j] = (__bf16)r2;
+  for (int k = 0; k < 4; ++k) {
+    const float a = v[2 * k], b = v[2 * k + 1];
+    h[k] = cvt_pk_bf16(a, b);
+    const float ra = a - __uint_as_float(h[k] << 16), rb = b - __uint_as_float(h[k] & 0xFFFF0000u);
+    m[k] = cvt_pk_bf16(ra, rb);
+    const float sa = ra - __uint_as_float(m[k] << 16), sb = rb - __uint_as_float(m[k] & 0xFFFF0000u);
+    o[k] = cvt_pk_bf16(sa, sb);
   }
+  hi = __builtin_bit_cast(bf16x8, make_uint4(h[0], h[1], h[2], h[3]));
+  mid = __builtin_bit_cast(bf16x8, make_uint4(m[0], m[1], m[2], m[3]));
+  lo = __builtin_bit_cast(bf16x8, make_uint4(o[0], o[1], o[2], o[3]));
 }
 
 __device__ inline floatx4 mfma3(bf16x8 a, bf16x8 bhi, bf16x8 bmid, bf16x8 blo) {
