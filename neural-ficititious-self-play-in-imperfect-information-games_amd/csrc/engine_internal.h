@@ -93,7 +93,7 @@ struct Memories {
 //             (the layer-1 K slots 8g..8g+7 of lane row g)
 //   ba[g][i]  the same bits of input i's 32-bit mask over the minibatch's 32 samples (the
 //             bit-transposed minibatch: the dW1 = X^T dZ1 operand)
-//   tg[s]     sample s's three fit targets and the step's learning rate
+//   tg[s]     sample s's three fit targets (AR: divided by the batch, exact) and the step's lr
 // Input 30 (CHAIN_BIAS_BIT) is the constant 1 of every sample: the chain keeps b1 as W1's
 // row 30, so the layer-1 products include the bias and dW1's row 30 is gb1.
 constexpr uint32_t CHAIN_BIAS_BIT = 1u << 30;

@@ -245,8 +245,10 @@ __global__ void __launch_bounds__(128) k_ar_prep(PrepArgs P) {
     }
     __syncthreads();
     const bool in = b < P.B;
-    emit_recs(P.LB.ar_rec + (slot_u * P.E + e) * (P.B / CHAIN_MB), in ? px[b] : 0u, in ? pt[b][0] : 0.f,
-              in ? pt[b][1] : 0.f, in ? pt[b][2] : 0.f, P.lr_ar, P.B);
+    // targets / batch: the AR chain's cross-entropy gradient takes them pre-scaled (exact)
+    const float sc = 1.0f / (float)CHAIN_MB;
+    emit_recs(P.LB.ar_rec + (slot_u * P.E + e) * (P.B / CHAIN_MB), in ? px[b] : 0u, in ? pt[b][0] * sc : 0.f,
+              in ? pt[b][1] * sc : 0.f, in ? pt[b][2] * sc : 0.f, P.lr_ar, P.B);
     __syncthreads();
   }
   if (last && b < P.B) P.M.dbg_rows[dbg * P.B + b] = cand[b];
@@ -664,13 +666,16 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
         const float eps = 1e-7f, hi = 1.0f - 1e-7f;
         const float q0 = y0 * rS, q1 = y1 * rS, q2 = y2 * rS;
         p_keep[0] = q0; p_keep[1] = q1; p_keep[2] = q2;
-        const float m0 = (q0 >= eps && q0 <= hi) ? tt[0] : 0.f;
-        const float m1 = (q1 >= eps && q1 <= hi) ? tt[1] : 0.f;
-        const float m2 = (q2 >= eps && q2 <= hi) ? tt[2] : 0.f;
-        const float k = ((m0 + m1) + m2) * (rS * invm);
-        d0 = y0 * k - m0 * invm;
-        d1 = y1 * k - m1 * invm;
-        d2 = y2 * k - m2 * invm;
+        // q in [eps, 1 - eps]  <=>  clamp(q, eps, 1 - eps) == q
+        const float m0 = __builtin_amdgcn_fmed3f(q0, eps, hi) == q0 ? tt[0] : 0.f;
+        const float m1 = __builtin_amdgcn_fmed3f(q1, eps, hi) == q1 ? tt[1] : 0.f;
+        const float m2 = __builtin_amdgcn_fmed3f(q2, eps, hi) == q2 ? tt[2] : 0.f;
+        // AR records carry t / batch (k_ar_prep; a power-of-two scale, exact), so the 1 / batch
+        // of both terms is already in m_k
+        const float k = ((m0 + m1) + m2) * rS;
+        d0 = y0 * k - m0;
+        d1 = y1 * k - m1;
+        d2 = y2 * k - m2;
       }
     }
     if (LOSS) {            // fit loss of this minibatch (before its update), Keras' epoch mean
@@ -684,7 +689,8 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
         Ls = acc * (1.0f / 3.0f);
       } else {             // categorical cross-entropy: -sum t log(clip(y / S))
         float acc = 0.f;
-        for (int k = 0; k < 3; ++k) acc -= tt_keep[k] * __logf(fminf(fmaxf(p_keep[k], 1e-7f), 1.0f - 1e-7f));
+        for (int k = 0; k < 3; ++k)      // (tt_keep = t / batch)
+          acc -= (tt_keep[k] * (float)CHAIN_MB) * __logf(fminf(fmaxf(p_keep[k], 1e-7f), 1.0f - 1e-7f));
         Ls = acc;
       }
       float x = (g & 1) == 0 ? Ls : 0.f;     // the 32 distinct samples: rows 0 and 2

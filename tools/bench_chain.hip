@@ -65,7 +65,8 @@ int main(int argc, char** argv) {
       const auto& r = fit[st * 32 + k];
       const uint32_t xb = r.x | CHAIN_BIAS_BIT;      // emit_recs: the bias input
       for (int g = 0; g < 4; ++g) rec[st].fa[g][k] = bits8_host(xb, g);
-      rec[st].tg[k] = make_float4(r.t0, r.t1, r.t2, lr);
+      const float ts = relu ? 1.f : 1.f / 32.f;        // AR records: targets / batch (k_ar_prep)
+      rec[st].tg[k] = make_float4(r.t0 * ts, r.t1 * ts, r.t2 * ts, lr);
       for (int i = 0; i <= CHAIN_BIAS_IN; ++i) if ((xb >> i) & 1u) xt[i] |= 1u << k;
     }
     for (int i = 0; i < 32; ++i)
