@@ -186,7 +186,10 @@ typedef struct nfsp_engine_cfg {
 typedef struct nfsp_engine_stats {
   int64_t hands, rollouts;
   int64_t rl_total[2], sl_total[2];     /* inserts ever, per agent */
-  int64_t rl_size[2], sl_size[2];       /* memory sizes (ReplayBuffer/ReservoirBuffer.size) */
+  int64_t rl_size[2], sl_size[2];       /* memory sizes (ReplayBuffer/ReservoirBuffer.size);
+                                         * sl_size counts the reservoir rows as stored: a
+                                         * rollout's SL inserts (in sl_total) are applied to
+                                         * them by nfsp_engine_update */
   int64_t last_rl[2], last_sl[2];       /* inserts of the last rollout */
   int64_t br_updates[2], ar_updates[2];
   int64_t iteration[2], target_syncs[2];

@@ -559,10 +559,11 @@ extern "C" int nfsp_engine_get_stats(nfsp_engine* e, nfsp_engine_stats* out) {
   out->hands = h.hands;
   out->rollouts = h.rollouts;
   for (int a = 0; a < 2; ++a) {
-    // before nfsp_engine_update has consumed a rollout its inserts are already in M_RL
+    // before nfsp_engine_update has consumed a rollout its inserts are already made: the
+    // RL ones are in M_RL, the SL ones wait in the pending list
     const int64_t rl_total = h.rl_total[a] + (e->pending_update ? h.last_rl[a] : 0);
     out->rl_total[a] = rl_total;
-    out->sl_total[a] = h.sl_total[a];
+    out->sl_total[a] = h.sl_total[a] + (e->pending_update ? h.last_sl[a] : 0);
     out->rl_size[a] = rl_total < e->cfg.rl_capacity ? rl_total : e->cfg.rl_capacity;
     out->sl_size[a] = h.sl_count[a];
     out->last_rl[a] = h.last_rl[a];

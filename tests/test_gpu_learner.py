@@ -1,0 +1,84 @@
+"""Whole learner steps (nfsp_engine_update) against the numpy restatement of the learner
+(oracle/learner_oracle.py).  Every update of the step is replayed:
+* BR: row sampling, target-net forwards, TD targets, the row-0 quirk and the proxy; the Huber
+  fits in their permutation order; the lr schedule; target syncs in mid-step;
+* AR: the reservoir as of each trigger; the cross-entropy fits;
+* the reservoir after the step.
+
+The engine's memories after the rollout are the input.  The rollout itself is checked
+against rollout_oracle in test_gpu_engine.py.
+
+Tolerances:
+* Sampling, schedules and the reservoir are compared exactly.
+* Weights are compared after ~60 updates (~480 SGD steps) per net: max 1e-4, median 1e-7.
+  Measured: max 2.4e-7, median 0. The chain sums exact products on bf16 matrix cores;
+  numpy sums with BLAS. The max leaves room for a ReLU input near zero to change sign
+  between the two.
+"""
+import numpy as np
+import pytest
+import torch
+
+import learner_oracle as LO
+
+CFG = dict(n_lanes=4096, rl_capacity=3000, sl_capacity=2000, target_every=30, seed=4242)
+
+
+def _bits(xf):
+    x = np.asarray(xf).reshape(len(xf), -1) != 0
+    return (x.astype(np.int64) << np.arange(x.shape[1])).sum(axis=1)
+
+
+def _snapshot(eng):
+    st = eng.stats()
+    out = []
+    for a in (0, 1):
+        m = {k: (v.cpu().numpy().copy() if torch.is_tensor(v) else v) for k, v in eng.memories(a).items()}
+        n_sl = int(st["last_sl"][a])
+        out.append(dict(
+            w={n: eng.get_weights(a, n) for n in (0, 1, 2)},
+            rl_total=int(st["rl_total"][a]), last_rl=int(st["last_rl"][a]),
+            sl_total=int(st["sl_total"][a]), last_sl=n_sl,
+            iteration=int(st["iteration"][a]), br_updates=int(st["br_updates"][a]),
+            epsilon=float(st["epsilon"][a]),
+            rl_s_bits=_bits(m["rl_s"]), rl_s2_bits=_bits(m["rl_s2"]), rl_a=m["rl_a"],
+            rl_r=m["rl_r"], rl_t=m["rl_t"],
+            sl_s_bits=_bits(m["sl_s"]), sl_a=m["sl_a"],
+            pend_x=m["pend_x"][:n_sl].astype(np.int64) & 0xFFFFFFFF, pend_a=m["pend_a"][:n_sl],
+            pend_pos=m["pend_pos"][:n_sl]))
+    return st, out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("quirks", [7, 0])
+def test_learner_step_matches_oracle(pkg, quirks):
+    eng = pkg.engine.SelfPlayEngine(init_seed=5, quirks=quirks, **CFG)
+    for _ in range(2):
+        eng.step()
+    eng.rollout()
+    st0, state = _snapshot(eng)
+    eng.update()
+    st1 = eng.stats()
+    c = eng.cfg
+    cfg = dict(c=c.inserts_per_update, batch=c.batch, epochs=c.epochs, rl_capacity=c.rl_capacity,
+               sl_capacity=c.sl_capacity, target_every=c.target_every, lr_br=c.lr_br, lr_ar=c.lr_ar,
+               gamma=c.gamma, seed=c.seed)
+    want = LO.learner_step(cfg, state, quirks=quirks)
+    for a in (0, 1):
+        W = want[a]
+        assert W["U_br"] > 2 * c.target_every // 2 and W["U"] >= W["U_br"]     # several segments
+        assert st1["br_updates"][a] == W["br_updates"]
+        assert st1["ar_updates"][a] - st0["ar_updates"][a] == W["ar_updates"]
+        assert st1["iteration"][a] == W["iteration"]
+        assert st1["epsilon"][a] == pytest.approx(W["epsilon"], rel=1e-12)
+        assert st1["lr_br"][a] == pytest.approx(W["lr_br"], rel=1e-7)
+        assert st1["temp"][a] == pytest.approx(W["temp"], rel=1e-12)
+        assert st1["exploitability"][a] == pytest.approx(W["exploitability"], abs=1e-4)
+        for n in (0, 1, 2):
+            d = np.abs(eng.get_weights(a, n) - W["w"][n])
+            assert d.max() <= 1e-4, (a, n, d.max())
+            assert np.median(d) <= 1e-7, (a, n, np.median(d))
+        m = eng.memories(a)
+        size = int(st1["sl_size"][a])
+        assert np.array_equal(_bits(m["sl_s"].cpu().numpy()[:size]), W["res_x"][:size])
+        assert np.array_equal(m["sl_a"].cpu().numpy()[:size], W["res_a"][:size])
