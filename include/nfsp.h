@@ -92,7 +92,11 @@ int nfsp_num_envs(const nfsp_ctx* ctx);
 /* ---------------------------------------------------------------- env (batched newenv API) */
 /* Stores deals (P0, P1, public rank; rank 0 = Ace is best) for the NEXT nfsp_env_reset.
  * Test/host injection of the deck (the reference shuffles the global `random`,
- * leduc/deck.py:42-50; the Python drop-in shuffles there and injects the result). */
+ * leduc/deck.py:42-50; the Python drop-in shuffles there and injects the result).
+ * This is how the deal modes of SURVEY §8(b) reach the device.  PHILOX is
+ * nfsp_env_reset's own draw.  PY3_MT and PY2_MT are CPython 3 / 2.7 shuffles of the
+ * host's MT19937 stream (nfsp_amd.pyrandom.set_python_semantics(3 | 2)), drawn on the host
+ * and injected here. */
 int nfsp_env_set_deal(nfsp_ctx* ctx, const uint8_t* dev_ranks /* [n,3] */);
 /* Env.reset(dealer) (leduc/newenv.py:76-114) for every env.  Deal = the pending
  * nfsp_env_set_deal if any, else a Philox draw keyed by (seed, env, reset index). */

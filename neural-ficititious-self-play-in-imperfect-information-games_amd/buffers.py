@@ -23,6 +23,7 @@ import numpy as np
 import torch
 
 from . import native
+from . import pyrandom
 
 OBS = 30
 
@@ -149,7 +150,7 @@ class ReplayBuffer(_DeviceMemory):
         """``sample_batch`` returning the batch as device tensors (s [k,30], a [k,3],
         r [k], s2 [k,30], t [k])."""
         k = min(self.count, batch_size)
-        logical = random.sample(range(self.count), k)
+        logical = pyrandom.sample(range(self.count), k)
         dev_pos, dev_slot, pen_pos, pen = self._logical_rows(logical)
         out = _Table(k, True, self.dev)
         if dev_slot:
@@ -193,7 +194,7 @@ class ReservoirBuffer(_DeviceMemory):
             slot = self.count
             self.count += 1
         else:
-            j = random.randrange(1, self.buffer_size + 1)
+            j = pyrandom.randrange(1, self.buffer_size + 1)
             if j >= self.buffer_size:
                 return
             slot = j
@@ -201,7 +202,7 @@ class ReservoirBuffer(_DeviceMemory):
 
     def sample_device(self, batch_size):
         k = min(self.count, batch_size)
-        return self._gather(random.sample(range(self.count), k))
+        return self._gather(pyrandom.sample(range(self.count), k))
 
     def sample_batch(self, batch_size):
         o = self.sample_device(batch_size)

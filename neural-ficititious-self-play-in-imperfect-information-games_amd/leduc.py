@@ -31,6 +31,7 @@ import numpy as np
 import torch
 
 from . import native
+from . import pyrandom
 
 # numpy view of the device `Hand` struct (csrc/nfsp_device.h), 64 bytes
 HAND_DTYPE = np.dtype([
@@ -52,7 +53,7 @@ def bits_to_obs(b: int) -> np.ndarray:
 def deal_from_global_random():
     """One reference-deck shuffle with the global ``random`` (leduc/deck.py:35-44)."""
     cards = list(range(6))          # deck order r0s0 r0s1 r1s0 r1s1 r2s0 r2s1
-    random.shuffle(cards)
+    pyrandom.shuffle(cards)        # Python 3 (default) or 2.7 semantics: pyrandom
     return cards[5] >> 1, cards[4] >> 1, cards[3] >> 1
 
 

@@ -14,6 +14,7 @@ import numpy as np
 
 from .agent import CFG, Agent
 from .leduc import Env
+from . import pyrandom
 
 
 def play_hand(env, players, dealer, eta):
@@ -40,7 +41,7 @@ def play_hand(env, players, dealer, eta):
 def train(env, player1, player2, episodes=400000, eta=0.1, stats_every=100):
     """Returns the exploitability-proxy curve main.train plots (main.py:73-75,122)."""
     players = [player1, player2]
-    dealer = random.randint(0, 1)
+    dealer = pyrandom.randint(0, 1)
     curve = []
     for i in range(episodes):
         dealer = 1 - dealer

@@ -1,0 +1,75 @@
+"""The drop-in's Python-semantics switch (nfsp_amd.pyrandom; SURVEY §8(b) deal_mode).
+
+Mode 3 is CPython 3's ``random`` itself, which the golden fixtures pin.  Mode 2 restates
+CPython 2.7's integer methods (Lib/random.py 2.7: ``int(random() * n)``).  There is no
+Python 2 in the image, so mode 2 is checked against that published algorithm draw for draw
+(parity unpinned otherwise).
+"""
+import random
+
+import pytest
+
+
+@pytest.fixture
+def pr(pkg):
+    m = pkg.pyrandom
+    yield m
+    m.set_python_semantics(3)
+
+
+def test_mode3_is_cpython3(pr):
+    pr.set_python_semantics(3)
+    random.seed(11)
+    a = list(range(6)); pr.shuffle(a)
+    s = pr.sample(range(40000), 128)
+    r = pr.randrange(1, 40001)
+    d = pr.randint(0, 1)
+    random.seed(11)
+    b = list(range(6)); random.shuffle(b)
+    assert a == b and s == random.sample(range(40000), 128)
+    assert r == random.randrange(1, 40001) and d == random.randint(0, 1)
+
+
+def test_mode2_follows_python27(pr):
+    pr.set_python_semantics(2)
+    random.seed(1234)
+    a = list(range(6)); pr.shuffle(a)
+    small = pr.sample(range(200), 128)          # n <= setsize (21 + 4^5): pool branch
+    big = pr.sample(range(40000), 128)          # set branch
+    ri = pr.randint(0, 1)
+    rr = pr.randrange(1, 40001)
+    random.seed(1234)
+    u = random.random
+    b = list(range(6))
+    for i in range(5, 0, -1):                   # one draw per swap
+        j = int(u() * (i + 1))
+        b[i], b[j] = b[j], b[i]
+    pool, want_small = list(range(200)), []
+    for i in range(128):
+        j = int(u() * (200 - i))
+        want_small.append(pool[j])
+        pool[j] = pool[200 - i - 1]
+    seen, want_big = set(), []
+    for _ in range(128):
+        j = int(u() * 40000)
+        while j in seen:
+            j = int(u() * 40000)
+        seen.add(j)
+        want_big.append(j)
+    assert a == b and small == want_small and big == want_big
+    assert ri == int(u() * 2) and rr == 1 + int(u() * 40000)
+
+
+def test_dropin_deal_follows_the_mode(pr, pkg):
+    leduc = pkg.leduc
+    for mode in (3, 2):
+        pr.set_python_semantics(mode)
+        random.seed(5)
+        got = [leduc.deal_from_global_random() for _ in range(20)]
+        random.seed(5)
+        want = []
+        for _ in range(20):
+            cards = list(range(6))
+            pr.shuffle(cards)
+            want.append((cards[5] >> 1, cards[4] >> 1, cards[3] >> 1))
+        assert got == want
