@@ -18,7 +18,9 @@ scaling); a barrier and a max-over-ranks of the elapsed time bracket the timed r
 
 Roofline: HIP events recorded on the engine's stream around every kernel launch give
 each kernel's average duration; the dominant kernel's algorithmic FLOPs (or bytes) per
-launch / that duration is `roofline.achieved`.
+launch / that duration is `roofline.achieved`.  The chains are latency-bound SGD steps: they
+are priced in MFMA FLOPs, and `roofline_other.k_chain3_br_hbm` gives the same kernel in
+SURVEY 8(d)'s HBM framing (128 sampled M_RL tuples x 257 B per update).
 
 `cpu_baseline` (rank 0, N = 1 only) comes from the C++ restatement of the reference's
 main.train (oracle/nfsp_cpu.cpp).  It uses the reference cadence and this config's memory
@@ -225,9 +227,19 @@ def main():
         return {"kernel": name, "bound": "mfma", "achieved": ach, "peak": PEAK_FP32_TFLOPS,
                 "unit": "TFLOP/s", "frac": ach / PEAK_FP32_TFLOPS, "traffic": None,
                 "avg_ms": k_ms[name], "launches": k_launches[name], "flop_per_launch": flop}
+    def chain_roof_hbm(name, updates, tuple_bytes):
+        """SURVEY 8(d)'s HBM framing of a chain: algorithmic bytes = the 128 sampled memory
+        tuples of each update (reference fp32 layout), per launch."""
+        n = max(k_launches[name], 1)
+        byt = updates * 128 * tuple_bytes / n
+        ach = byt / (k_ms[name] * 1e-3) / 1e9 if k_ms[name] > 0 else 0.0
+        return {"kernel": name, "bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS,
+                "unit": "GB/s", "frac": ach / PEAK_HBM_GBS, "traffic": load_pmc(args.config, name),
+                "avg_ms": k_ms[name], "launches": k_launches[name], "bytes_per_launch": byt}
     roofs = {"k_chain3_br": chain_roof("k_chain3_br", br_upd),
              "k_chain3_ar": chain_roof("k_chain3_ar", ar_upd),
-             "k_rollout": roof_rollout}
+             "k_rollout": roof_rollout,
+             "k_chain3_br_hbm": chain_roof_hbm("k_chain3_br", br_upd, BYTES_RL)}
     # the dominant kernel = largest GPU time inside the timed region
     singles = [k for k in timings if k != "learner"]
     dom = max(singles, key=lambda k: timings[k][0])
@@ -254,7 +266,8 @@ def main():
                    "rl_capacity": cfg["rl_capacity"], "sl_capacity": cfg["sl_capacity"],
                    "inserts_per_update": 128, "batch": 128, "parallelism": f"replicas x{world}"},
         "roofline": roofline,
-        "roofline_other": {k: v for k, v in roofs.items() if k != roofline["kernel"]},
+        "roofline_other": {k: v for k, v in roofs.items() if k != roofline["kernel"]},   # incl. the
+        # dominant chain's HBM framing (k_chain3_br_hbm: SURVEY 8(d) bytes, PMC traffic)
         "kernel_ms": k_ms,
         "rollout_only_hands_per_s": cfg["n_lanes"] / (rollout_path_ms * 1e-3) * world,
         "per_step": {"br_updates": br_upd / args.steps, "ar_updates": ar_upd / args.steps,
