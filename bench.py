@@ -48,6 +48,8 @@ CONFIGS = {
     "c2": dict(n_lanes=65_536, rl_capacity=40_000, sl_capacity=40_000,
                label="C2: 65,536 Leduc lanes/GPU, M_RL/M_SL 40k, eta 0.1, 2x64 MLP heads, "
                      "reference update cadence"),
+    "c5": dict(n_lanes=1_048_576, rl_capacity=200_000, sl_capacity=2_000_000, game="kuhn",
+               label="C5: Kuhn swap-in, 1,048,576 lanes/GPU, C3's memories and cadence"),
 }
 
 PEAK_FP32_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA peak
@@ -76,13 +78,14 @@ def load_pmc(config, kernel):
     return None if k is None else k.get("hbm_bytes_per_launch")
 
 
-def cpu_baseline_numpy(seconds: float):
+def cpu_baseline_numpy(seconds: float, game: str = "leduc"):
     """The reference-structured CPU path in numpy: oracle Env/Agent + main.train's loop."""
     import random
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import nfsp_oracle as orc
     random.seed(0)
     env, p1, p2 = orc.make_main(init_seed=0)
+    env.kuhn = game == "kuhn"
     players = [p1, p2]
     dealer = random.randint(0, 1)
     hands = 0
@@ -107,14 +110,14 @@ def cpu_baseline(seconds: float, threads: int, cfg: dict):
     import cpu_port
     if not os.path.exists(cpu_port.LIB_PATH):
         subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle")], check=True)
-    c = cpu_port.make_cfg(None, 0, True, "leduc", rl_capacity=cfg["rl_capacity"],
+    c = cpu_port.make_cfg(None, 0, True, cfg.get("game", "leduc"), rl_capacity=cfg["rl_capacity"],
                           sl_capacity=cfg["sl_capacity"])
     one, el1 = cpu_port.bench(c, 1, min(seconds, 5.0))
     hands, el = cpu_port.bench(c, threads, seconds)
     return {"value": hands / el, "unit": "hands/s", "cores": threads, "kind": "port",
             "per_core": one / el1,
             "sample": f"{hands} hands of main.train restated in C++ (oracle/nfsp_cpu.cpp: the "
-                      f"reference's Env, scheduler, memories M_RL {cfg['rl_capacity']:,} / M_SL "
+                      f"reference's {cfg.get('game', 'leduc').capitalize()} Env, scheduler, memories M_RL {cfg['rl_capacity']:,} / M_SL "
                       f"{cfg['sl_capacity']:,}, updates at the reference cadence, fp32 MLPs) by "
                       f"{threads} independent replicas (one learner each) in {el:.1f} s; one "
                       f"replica alone: {one / el1:,.0f} hands/s"}
@@ -189,9 +192,10 @@ def main():
     import __graft_entry__
     pkg = __graft_entry__.load_package()
     cfg = CONFIGS[args.config]
+    game = pkg.native.GAME_KUHN if cfg.get("game") == "kuhn" else pkg.native.GAME_LEDUC
     eng = pkg.engine.SelfPlayEngine(n_lanes=cfg["n_lanes"], rl_capacity=cfg["rl_capacity"],
                                     sl_capacity=cfg["sl_capacity"], seed=1234 + rank,
-                                    init_seed=rank)
+                                    init_seed=rank, game=game)
     for _ in range(args.warmup):
         eng.step()
     torch.cuda.synchronize()
@@ -250,7 +254,7 @@ def main():
         roofline["traffic_source"] = f"profiles/pmc_{args.config}.json (rocprofv3 --pmc passes)"
     rollout_path_ms = k_ms["k_rollout"] + k_ms["k_scan"] + k_ms["k_commit"]
     out = {
-        "metric": "Leduc self-play hands/sec",
+        "metric": "Kuhn self-play hands/sec" if cfg.get("game") == "kuhn" else "Leduc self-play hands/sec",
         "value": value,
         "unit": "hands/s",
         "n_gpus": world,
@@ -282,7 +286,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, threads, cfg)
-        out["cpu_baseline_numpy"] = cpu_baseline_numpy(min(args.cpu_seconds, 5.0))
+        out["cpu_baseline_numpy"] = cpu_baseline_numpy(min(args.cpu_seconds, 5.0), cfg.get("game", "leduc"))
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
