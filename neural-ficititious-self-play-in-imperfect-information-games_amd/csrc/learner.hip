@@ -425,14 +425,17 @@ __device__ inline float sum_x16(float x) {
 // (K = 32 covers all 30 inputs).  Per wave (hidden slice 16w..16w+15, lane (g, c) =
 // (l >> 4, l & 15)):
 //   * layer-1 K slot 8g + j <-> input pi(g, j) = 4g + j (j < 4) or 16 + 4g + j - 4, so the
-//     dW1 accumulator lands in the registers that hold W1 (wr[j] = W1[pi(g, j)][16w + c]);
+//     dW1 accumulator lands in the registers that hold W1 (wr[j] = W1[pi(g, j)][16w + c]).
+//     Input 30 is the constant 1 (CHAIN_BIAS_BIT).  Its row holds b1, so the layer-1
+//     products include the bias, and dW1's row 30 is gb1;
 //   * forward twice from the same registers: Z1 sample-major (D row = sample, for the
 //     backward and dW1) and Z1^T hidden-major (D row = hidden: layer 2 is then 4 lane-local
 //     FMAs per output plus two permlane swaps instead of a 16-lane reduction);
 //   * dW1 = X^T dZ1 with K = samples (K slot 8g + j <-> sample 16 (j >> 2) + 4g + (j & 3));
 //   * every bit operand comes ready-made from the step record (StepRec: the prep kernels
-//     expand the masks and their bit transpose), loaded three steps ahead into four named
-//     buffers (loop unrolled by four: no load result is ever copied);
+//     expand the masks and their bit transpose).  Records pass through a 4-slot LDS ring:
+//     each wave loads a quarter of record t + 2 during step t, and step t + 1's barrier
+//     publishes it;
 //   * one barrier per step (the 4 waves' layer-2 partials); all other exchange is
 //     wave-private (LDS dm / w2t) or cross-lane (DPP, permlane).
 // ---------------------------------------------------------------------------
