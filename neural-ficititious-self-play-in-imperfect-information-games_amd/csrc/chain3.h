@@ -1,0 +1,493 @@
+// The SGD chain kernel (k_chain3) and its helpers, shared by the two translation units that
+// instantiate it: learner.hip (BR, k_chain3<1, *>) and chain_ar.hip (AR, k_chain3<0, *>).
+// The two are compiled with different scheduler flags (__graft_entry__.FILE_FLAGS).
+#pragma once
+#include "engine_internal.h"
+
+namespace nfsp {
+namespace chain {
+namespace nn = nfsp::nn;
+using namespace nfsp::eng;
+
+// ---------------------------------------------------------------------------
+// SGD chains: one workgroup (4 waves) per (agent, net) runs that net's updates back to
+// back with the whole net in registers (k_chain3).  Reference: agent/agent.py:241-264
+// (model.fit(batch_size=32, epochs=2) of the BR Q-net and the AR policy net).
+// ---------------------------------------------------------------------------
+struct ChainArgs {
+  float* w[2];                    // weights of (agent, net)
+  float* sync_to[2];              // BR: target net to copy into at the end (or null)
+  const StepRec* rec;             // [2][umax][E][B / 32] step records (prep kernels)
+  const uint8_t* active;          // AR: per-update flag, 0..0 1..1 in u (null for BR)
+  int64_t umax;
+  int64_t u0[2], u1[2];           // update range per agent
+  int agents[2];                  // blockIdx -> agent
+  int B, E;
+  unsigned long long* stamps;     // diagnostic build only (NFSP_CHAIN_STAMPS): phase cycles
+  float* loss_out;                // optional: [2][umax][E] Keras epoch losses (the values the
+                                  // reference's TensorBoard callbacks log, agent/agent.py:84-88)
+};
+
+// In-kernel phase stamps (cdna_hip_programming.md §7): a separate diagnostic build only.
+#ifdef NFSP_CHAIN_STAMPS
+#define CHAIN_STAMP(k)                                                                   \
+  do {                                                                                  \
+    __builtin_amdgcn_sched_barrier(0);                                                  \
+    unsigned long long _t;                                                              \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");          \
+    __builtin_amdgcn_sched_barrier(0);                                                  \
+    st_acc[k] += _t - st_last;                                                          \
+    st_last = _t;                                                                       \
+  } while (0)
+#else
+#define CHAIN_STAMP(k) do { } while (0)
+#endif
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+__device__ inline float dpp_f(float x, int ctrl) {
+  switch (ctrl) {   // the control word must be an immediate
+    case 0x128: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x128, 0xF, 0xF, false));
+    case 0xB1: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0xB1, 0xF, 0xF, false));
+    case 0x4E: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x4E, 0xF, 0xF, false));
+    default: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x141, 0xF, 0xF, false));
+  }
+}
+
+__device__ inline float dpp_any(float x, int ctrl) {
+  switch (ctrl) {
+    case 0x121: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x121, 0xF, 0xF, false));
+    case 0x122: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x122, 0xF, 0xF, false));
+    case 0x124: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x124, 0xF, 0xF, false));
+    default: return dpp_f(x, ctrl);
+  }
+}
+
+// x + partner(lane ^ 32) in every lane
+__device__ inline float sum_x32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// x + partner(lane ^ 16) in every lane
+__device__ inline float sum_x16(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// ---------------------------------------------------------------------------
+// k_chain3: the SGD chain on bf16 matrix cores with exact-f32 operands.
+//
+// An f32 value v is split exactly into three bf16 terms v = hi + mid + lo (8 + 8 + 8
+// significand bits, round-to-nearest at each cut), and a Leduc observation is 0/1, so
+// X.W = X.lo + X.mid + X.hi with every product exact and f32 accumulation: the 16 chained
+// v_mfma_f32_16x16x4_f32 of a layer-1 product become 3 v_mfma_f32_16x16x32_bf16 per tile
+// (K = 32 covers all 30 inputs).  Per wave (hidden slice 16w..16w+15, lane (g, c) =
+// (l >> 4, l & 15)):
+//   * layer-1 K slot 8g + j <-> input pi(g, j) = 4g + j (j < 4) or 16 + 4g + j - 4, so the
+//     dW1 accumulator lands in the registers that hold W1 (wr[j] = W1[pi(g, j)][16w + c]).
+//     Input 30 is the constant 1 (CHAIN_BIAS_BIT).  Its row holds b1, so the layer-1
+//     products include the bias, and dW1's row 30 is gb1;
+//   * forward twice from the same registers: Z1 sample-major (D row = sample, for the
+//     backward and dW1) and Z1^T hidden-major (D row = hidden: layer 2 is then 4 lane-local
+//     FMAs per output plus two permlane swaps instead of a 16-lane reduction);
+//   * dW1 = X^T dZ1 with K = samples (K slot 8g + j <-> sample 16 (j >> 2) + 4g + (j & 3));
+//   * every bit operand comes ready-made from the step record (StepRec: the prep kernels
+//     expand the masks and their bit transpose).  Records pass through a 4-slot LDS ring:
+//     each wave loads a quarter of record t + 2 during step t, and step t + 1's barrier
+//     publishes it;
+//   * one barrier per step (the 4 waves' layer-2 partials); all other exchange is
+//     wave-private (LDS dm / w2t) or cross-lane (DPP, permlane).
+// ---------------------------------------------------------------------------
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+#ifdef NFSP_CHAIN_STAMPS
+// diagnostic build: [AR blk 0, AR blk 1, BR, -][wave][phase 0-5, -, -, kernel cycles, steps]
+static __device__ unsigned long long g_chain_stamps[4][4][10];
+#endif
+
+// Stores are unconditional: lanes whose copy is redundant (the odd lane rows of po / dm, the
+// rows g > 0 of w2t, the lanes past a record quarter) write to sink rows nobody reads, so
+// the loop has no exec-mask branches.
+struct Chain3Smem {
+  float po[2][4][64][4];     // per-wave partial layer-2 outputs by sample (rows 32..63: sink),
+                             // double-buffered by step parity
+  float dm[4][3][64];        // wave-private: dL/dz2 of the 32 samples, by output (32..63: sink)
+  float4 w2t[4][64];         // wave-private: W2[h][0..2] of the slice for Z1^T (lane l writes
+                             // row l; rows 0..15 are read)
+  StepRec ring[4];           // step records t .. t + 2 (slot t & 3), a quarter per wave
+  uint4 rec_sink[64];
+};
+constexpr int REC_CHUNKS = (int)(sizeof(StepRec) / 16);    // 288 x 16 B
+constexpr int REC_QUARTER = REC_CHUNKS / 4;                 // 72 per wave
+static_assert(REC_CHUNKS % 4 == 0 && REC_QUARTER > 64 && REC_QUARTER <= 128, "record chunking");
+// Reserve (nearly) all of a CU's LDS for a chain workgroup: a chain then has its CU to
+// itself -- no prep / target kernel's waves share its SIMDs.
+constexpr int CHAIN_LDS = 150 * 1024;
+static_assert(sizeof(Chain3Smem) <= CHAIN_LDS, "chain LDS");
+
+// exact three-term bf16 split of 8 f32 values, a pair at a time: one packed conversion
+// per pair and level (v_cvt_pk_bf16_f32, round to nearest even), the two f32 values of the
+// packed pair by shift / mask, and the two residuals.  v = hi + mid + lo exactly.
+// (inline asm: as plain conversions the compiler re-derives the low half by a second
+// single-value conversion instead of shifting the packed word)
+__device__ inline uint32_t cvt_pk_bf16(float a, float b) {
+  uint32_t r;
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ inline void split3(const float (&v)[8], bf16x8& hi, bf16x8& mid, bf16x8& lo) {
+#pragma clang fp contract(off)
+  uint32_t h[4], m[4], o[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float a = v[2 * k], b = v[2 * k + 1];
+    h[k] = cvt_pk_bf16(a, b);
+    const float ra = a - __uint_as_float(h[k] << 16), rb = b - __uint_as_float(h[k] & 0xFFFF0000u);
+    m[k] = cvt_pk_bf16(ra, rb);
+    const float sa = ra - __uint_as_float(m[k] << 16), sb = rb - __uint_as_float(m[k] & 0xFFFF0000u);
+    o[k] = cvt_pk_bf16(sa, sb);
+  }
+  hi = __builtin_bit_cast(bf16x8, make_uint4(h[0], h[1], h[2], h[3]));
+  mid = __builtin_bit_cast(bf16x8, make_uint4(m[0], m[1], m[2], m[3]));
+  lo = __builtin_bit_cast(bf16x8, make_uint4(o[0], o[1], o[2], o[3]));
+}
+
+__device__ inline floatx4 mfma3(bf16x8 a, bf16x8 bhi, bf16x8 bmid, bf16x8 blo) {
+  floatx4 z = {};
+  z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, blo, z, 0, 0, 0);
+  z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bmid, z, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bhi, z, 0, 0, 0);
+}
+__device__ inline floatx4 mfma3t(bf16x8 ahi, bf16x8 amid, bf16x8 alo, bf16x8 b) {
+  floatx4 z = {};
+  z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo, b, z, 0, 0, 0);
+  z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(amid, b, z, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, b, z, 0, 0, 0);
+}
+
+template <int RELU, int LOSS>
+__global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  Chain3Smem& sm = *reinterpret_cast<Chain3Smem*>(smem_raw);
+  const int a = C.agents[blockIdx.x];
+  const int tid = threadIdx.x;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l = tid & 63;
+  const int g = l >> 4, c = l & 15;
+  const int hid = 16 * w + c;
+  const int sl = 16 * (g >> 1) + c;            // this lane's loss sample
+  float* gw = C.w[blockIdx.x];
+  float wr[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int i = 16 * (j >> 2) + 4 * g + (j & 3);
+    wr[j] = i < nfsp::OBS ? gw[nn::OW1 + i * nn::H + hid] : i == CHAIN_BIAS_IN ? gw[nn::OB1 + hid] : 0.f;
+  }
+  float W2_0 = gw[nn::OW2 + 3 * hid + 0], W2_1 = gw[nn::OW2 + 3 * hid + 1], W2_2 = gw[nn::OW2 + 3 * hid + 2];
+  float b2_0 = gw[nn::OB2 + 0], b2_1 = gw[nn::OB2 + 1], b2_2 = gw[nn::OB2 + 2];
+  const int nmb = C.B / CHAIN_MB;
+  const int spu = C.E * nmb;                   // SGD steps per update
+  const float inv3m = 1.0f / (float)(3 * CHAIN_MB);
+  const float invm = 1.0f / (float)CHAIN_MB;
+  const int64_t slot0 = (int64_t)a * C.umax;
+  const int64_t u1 = C.u1[blockIdx.x];
+  int64_t u0 = C.u0[blockIdx.x];
+  if (C.active) {          // AR: skip the inactive prefix (M_SL <= batch; monotone in u)
+    while (u0 < u1) {
+      const int64_t q = u0 + l;
+      const unsigned long long m = __ballot(q < u1 && C.active[slot0 + q]);
+      if (m) { u0 += __builtin_ctzll(m); break; }
+      u0 += 64;
+    }
+    if (u0 > u1) u0 = u1;
+  }
+  const int T1 = (int)(u1 * spu);
+  int t = (int)(u0 * spu);
+  const uint4* recb = reinterpret_cast<const uint4*>(C.rec + slot0 * spu);
+  // this wave's quarter of record p (clamped), into two registers / back into ring slot p & 3;
+  // the lanes past the quarter load a duplicate chunk and store it to the sink
+  const bool in_q = l < REC_QUARTER - 64;
+  const int lb = in_q ? 64 + l : REC_QUARTER - 1;
+  auto issue = [&](int p, uint4& va, uint4& vb) {
+    const uint4* src = recb + (size_t)(p < T1 ? p : T1 - 1) * REC_CHUNKS + REC_QUARTER * w;
+    va = src[l];
+    vb = src[lb];
+  };
+  auto stash = [&](int p, const uint4& va, const uint4& vb) {
+    uint4* dst = reinterpret_cast<uint4*>(&sm.ring[p & 3]) + REC_QUARTER * w;
+    dst[l] = va;
+    *(in_q ? dst + 64 + l : &sm.rec_sink[l]) = vb;
+  };
+  auto publish = [&]() {   // this wave's W2 rows for its own Z1^T layer 2
+    sm.w2t[w][l] = make_float4(W2_0, W2_1, W2_2, 0.f);
+  };
+  const int prow = 32 * (g & 1) + sl;          // po / dm row: the sample, or the sink
+#ifdef NFSP_CHAIN_STAMPS
+  unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_last = 0;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
+  const unsigned long long st_t0 = st_last;
+#endif
+  // Records reach the lanes through an LDS ring: at step t each wave loads its quarter of
+  // record t + 2 and stores it at the end of step t; barrier(t + 1) publishes it.  Every
+  // load is consumed inside its own step (nothing loop-carried in registers), and the 4
+  // waves share one copy of each record.
+  float loss_acc = 0.f;                        // wave 0 lane 0: running epoch loss
+  auto step = [&]() {
+    uint4 va, vb;
+    issue(t + 2, va, vb);
+    const StepRec& R = sm.ring[t & 3];
+    const bf16x8 fa0 = __builtin_bit_cast(bf16x8, R.fa[g][c]);
+    const bf16x8 fa1 = __builtin_bit_cast(bf16x8, R.fa[g][16 + c]);
+    const bf16x8 ba0 = __builtin_bit_cast(bf16x8, R.ba[g][c]);
+    const bf16x8 ba1 = __builtin_bit_cast(bf16x8, R.ba[g][16 + c]);
+    // ---- layer 1, both orientations
+    bf16x8 whi, wmid, wlo;
+    split3(wr, whi, wmid, wlo);
+    float W2h[4][3];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float4 q = sm.w2t[w][4 * g + r];
+      W2h[r][0] = q.x; W2h[r][1] = q.y; W2h[r][2] = q.z;
+    }
+    // Z1^T first (layer 2 waits on it); Z1 (needed only by the backward) is issued after
+    // layer 2, so its matrix-core time overlaps the barrier wait
+    const floatx4 zh0 = mfma3t(whi, wmid, wlo, fa0);     // Z1^T: hidden 16w+4g+r, sample c
+    const floatx4 zh1 = mfma3t(whi, wmid, wlo, fa1);     //                      sample 16+c
+    __builtin_amdgcn_sched_barrier(0);
+    CHAIN_STAMP(0);
+    // ---- layer 2 partial over the slice, from Z1^T
+    float p0[3], p1[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { p0[k] = 0.f; p1[k] = 0.f; }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float h0 = fmaxf(zh0[r], 0.f);        // b1 is W1's row 30 (CHAIN_BIAS_IN)
+      const float h1 = fmaxf(zh1[r], 0.f);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        p0[k] = p0[k] + h0 * W2h[r][k];
+        p1[k] = p1[k] + h1 * W2h[r][k];
+      }
+    }
+    float q[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {   // rows g, g ^ 2 (tile halves), then g ^ 1
+      const auto rr = __builtin_amdgcn_permlane32_swap(__float_as_uint(p0[k]), __float_as_uint(p1[k]),
+                                                       false, false);
+      q[k] = sum_x16(__uint_as_float(rr[0]) + __uint_as_float(rr[1]));
+    }
+    const int buf = t & 1;
+    *reinterpret_cast<float4*>(&sm.po[buf][w][prow][0]) = make_float4(q[0], q[1], q[2], 0.f);
+    __builtin_amdgcn_sched_barrier(0);
+    const floatx4 zs0 = mfma3(fa0, whi, wmid, wlo);      // Z1: sample 4g+r, hidden 16w+c
+    const floatx4 zs1 = mfma3(fa1, whi, wmid, wlo);      //     sample 16+4g+r
+    const float4 tg = R.tg[sl];                          // read before the barrier pins it early
+    __builtin_amdgcn_sched_barrier(0);                   // ... and the Z1 MFMAs issue before it
+    CHAIN_STAMP(1);
+    __syncthreads();
+    CHAIN_STAMP(2);
+    // ---- output + loss of sample sl (every wave redundantly, identical results)
+    float d0, d1, d2, lr_step;
+    float o_keep[3], tt_keep[3], p_keep[3];     // for the optional loss log
+    {
+      const float4 a0 = *reinterpret_cast<const float4*>(&sm.po[buf][0][sl][0]);
+      const float4 a1 = *reinterpret_cast<const float4*>(&sm.po[buf][1][sl][0]);
+      const float4 a2 = *reinterpret_cast<const float4*>(&sm.po[buf][2][sl][0]);
+      const float4 a3 = *reinterpret_cast<const float4*>(&sm.po[buf][3][sl][0]);
+      const float o0 = (((a0.x + a1.x) + a2.x) + a3.x) + b2_0;
+      const float o1 = (((a0.y + a1.y) + a2.y) + a3.y) + b2_1;
+      const float o2 = (((a0.z + a1.z) + a2.z) + a3.z) + b2_2;
+      lr_step = tg.w;
+      const float tt[3] = {tg.x, tg.y, tg.z};
+      o_keep[0] = o0; o_keep[1] = o1; o_keep[2] = o2;
+      tt_keep[0] = tg.x; tt_keep[1] = tg.y; tt_keep[2] = tg.z;
+      if (RELU) {          // Huber on ReLU outputs, mean over 3 x batch
+        const float oz[3] = {o0, o1, o2};
+        float dd[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const float ee = tt[k] - fmaxf(oz[k], 0.f);
+          // |e| > 1 ? sign(e) : e  ==  clamp(e, -1, 1)
+          const float gg = __builtin_amdgcn_fmed3f(ee, -1.f, 1.f);
+          dd[k] = oz[k] > 0.f ? gg * -inv3m : 0.f;
+        }
+        d0 = dd[0]; d1 = dd[1]; d2 = dd[2];
+      } else {
+        // Keras categorical cross-entropy on the softmax (normalise p = y / S, clip p to
+        // [1e-7, 1 - 1e-7], loss -sum t log p; mean over the batch).  Its gradient w.r.t.
+        // the logits in closed form, with M = the unclipped outputs (the clip's gradient
+        // is 0 elsewhere) and T_M = sum_{k in M} t_k:
+        //   d_k = (y_k T_M / S - [k in M] t_k) / batch
+        // (the chain rule through normalise and softmax; the cancelling terms removed --
+        // oracle/nn_oracle.py evaluates the unsimplified chain)
+        const float mx = fmaxf(fmaxf(o0, o1), o2);
+        const float e0 = __expf(o0 - mx), e1 = __expf(o1 - mx), e2 = __expf(o2 - mx);
+        const float rs = __builtin_amdgcn_rcpf((e0 + e1) + e2);
+        const float y0 = e0 * rs, y1 = e1 * rs, y2 = e2 * rs;
+        const float rS = __builtin_amdgcn_rcpf((y0 + y1) + y2);
+        const float eps = 1e-7f, hi = 1.0f - 1e-7f;
+        const float q0 = y0 * rS, q1 = y1 * rS, q2 = y2 * rS;
+        p_keep[0] = q0; p_keep[1] = q1; p_keep[2] = q2;
+        // q in [eps, 1 - eps]  <=>  clamp(q, eps, 1 - eps) == q
+        const float m0 = __builtin_amdgcn_fmed3f(q0, eps, hi) == q0 ? tt[0] : 0.f;
+        const float m1 = __builtin_amdgcn_fmed3f(q1, eps, hi) == q1 ? tt[1] : 0.f;
+        const float m2 = __builtin_amdgcn_fmed3f(q2, eps, hi) == q2 ? tt[2] : 0.f;
+        // AR records carry t / batch (k_ar_prep; a power-of-two scale, exact), so the 1 / batch
+        // of both terms is already in m_k
+        const float k = ((m0 + m1) + m2) * rS;
+        d0 = y0 * k - m0;
+        d1 = y1 * k - m1;
+        d2 = y2 * k - m2;
+      }
+    }
+    if (LOSS) {            // fit loss of this minibatch (before its update), Keras' epoch mean
+      float Ls;
+      if (RELU) {          // huber_loss with py2's 1 / 2 == 0: |e| > 1 ? |e| : e^2 / 2, mean over 3
+        float acc = 0.f;
+        for (int k = 0; k < 3; ++k) {
+          const float e = tt_keep[k] - fmaxf(o_keep[k], 0.f);
+          acc += fabsf(e) > 1.0f ? fabsf(e) : 0.5f * e * e;
+        }
+        Ls = acc * (1.0f / 3.0f);
+      } else {             // categorical cross-entropy: -sum t log(clip(y / S))
+        float acc = 0.f;
+        for (int k = 0; k < 3; ++k)      // (tt_keep = t / batch)
+          acc -= (tt_keep[k] * (float)CHAIN_MB) * __logf(fminf(fmaxf(p_keep[k], 1e-7f), 1.0f - 1e-7f));
+        Ls = acc;
+      }
+      float x = (g & 1) == 0 ? Ls : 0.f;     // the 32 distinct samples: rows 0 and 2
+      x = x + dpp_any(x, 0x128);
+      x = x + dpp_any(x, 0x124);
+      x = x + dpp_any(x, 0x122);
+      x = x + dpp_any(x, 0x121);
+      x = sum_x32(sum_x16(x));
+      if (w == 0 && l == 0) {
+        const int in_u = t % spu;
+        loss_acc += x * invm;
+        if (in_u % nmb == nmb - 1) {
+          const int64_t uu = t / spu, ee = in_u / nmb;
+          C.loss_out[(slot0 + uu) * C.E + ee] = loss_acc / (float)nmb;
+          loss_acc = 0.f;
+        }
+      }
+    }
+    sm.dm[w][0][prow] = d0;
+    sm.dm[w][1][prow] = d1;
+    sm.dm[w][2][prow] = d2;
+    float gb2[3] = {d0, d1, d2};     // sum over the 32 samples: the row's 16, then rows g ^ 2
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      float x = gb2[k];
+      x = x + dpp_any(x, 0x128);
+      x = x + dpp_any(x, 0x124);
+      x = x + dpp_any(x, 0x122);
+      x = x + dpp_any(x, 0x121);
+      gb2[k] = sum_x32(x);
+    }
+    CHAIN_STAMP(3);
+    // ---- backward in the sample-major layout: samples 16 mt + 4g + r, hidden 16w + c
+    float4 dA[3], dB[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      dA[k] = *reinterpret_cast<const float4*>(&sm.dm[w][k][4 * g]);
+      dB[k] = *reinterpret_cast<const float4*>(&sm.dm[w][k][16 + 4 * g]);
+    }
+    float dz[8];
+    float g2_0 = 0.f, g2_1 = 0.f, g2_2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int r = j & 3;
+      const float z = j < 4 ? zs0[r] : zs1[r];
+      const float4 e0 = j < 4 ? dA[0] : dB[0], e1 = j < 4 ? dA[1] : dB[1], e2 = j < 4 ? dA[2] : dB[2];
+      const float x0 = r == 0 ? e0.x : r == 1 ? e0.y : r == 2 ? e0.z : e0.w;
+      const float x1 = r == 0 ? e1.x : r == 1 ? e1.y : r == 2 ? e1.z : e1.w;
+      const float x2 = r == 0 ? e2.x : r == 1 ? e2.y : r == 2 ? e2.z : e2.w;
+      const float h = fmaxf(z, 0.f);
+      g2_0 += h * x0;
+      g2_1 += h * x1;
+      g2_2 += h * x2;
+      const float dh = (x0 * W2_0 + x1 * W2_1) + x2 * W2_2;
+      dz[j] = z > 0.f ? dh : 0.f;
+    }
+    bf16x8 dhi, dmid, dlo;
+    split3(dz, dhi, dmid, dlo);
+    // dW1[16 it + 4g + r][16w + c] = sum over the 32 samples in dz's K order (row 30: gb1)
+    const floatx4 gA = mfma3(ba0, dhi, dmid, dlo);
+    const floatx4 gB = mfma3(ba1, dhi, dmid, dlo);
+    g2_0 = sum_x16(sum_x32(g2_0));
+    g2_1 = sum_x16(sum_x32(g2_1));
+    g2_2 = sum_x16(sum_x32(g2_2));
+    CHAIN_STAMP(4);
+    const float lr = lr_step;
+    W2_0 = W2_0 - lr * g2_0;
+    W2_1 = W2_1 - lr * g2_1;
+    W2_2 = W2_2 - lr * g2_2;
+    b2_0 = b2_0 - lr * gb2[0];
+    b2_1 = b2_1 - lr * gb2[1];
+    b2_2 = b2_2 - lr * gb2[2];
+    publish();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      wr[r] = wr[r] - lr * gA[r];
+      wr[4 + r] = wr[4 + r] - lr * gB[r];
+    }
+    stash(t + 2, va, vb);
+    CHAIN_STAMP(5);
+  };
+  if (t < T1) {
+    {
+      uint4 va, vb;
+      issue(t, va, vb);
+      stash(t, va, vb);
+      issue(t + 1, va, vb);
+      stash(t + 1, va, vb);
+    }
+    publish();
+    __syncthreads();
+    // drain the prologue's loads: the loop header then merges no pending load into the
+    // registers the loop reuses (else every step waits on its fresh record load)
+    __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0) (gfx9 encoding: expcnt 7, lgkmcnt 15)
+    for (; t < T1; ++t) step();
+  }
+#ifdef NFSP_CHAIN_STAMPS
+  if (l == 0) {
+    unsigned long long t_end;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_end)::"memory");
+    st_acc[8] = t_end - st_t0;
+    st_acc[9] = (unsigned long long)(T1 - (int)(u0 * spu));
+    if (C.stamps) {
+      for (int k = 0; k < 10; ++k) C.stamps[(blockIdx.x * 4 + w) * 10 + k] = st_acc[k];
+    } else {       // engine build: accumulate per (net, block, wave) for nfsp_debug_chain_stamps
+      for (int k = 0; k < 10; ++k) atomicAdd(&g_chain_stamps[RELU * 2 + blockIdx.x][w][k], st_acc[k]);
+    }
+  }
+#endif
+  float* dsts[2] = {gw, C.sync_to[blockIdx.x]};
+  for (int k = 0; k < 2; ++k) {
+    float* dst = dsts[k];
+    if (!dst) continue;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int i = 16 * (j >> 2) + 4 * g + (j & 3);
+      if (i < nfsp::OBS) dst[nn::OW1 + i * nn::H + hid] = wr[j];
+      else if (i == CHAIN_BIAS_IN) dst[nn::OB1 + hid] = wr[j];
+    }
+    if (g == 0) {
+      dst[nn::OW2 + 3 * hid + 0] = W2_0;
+      dst[nn::OW2 + 3 * hid + 1] = W2_1;
+      dst[nn::OW2 + 3 * hid + 2] = W2_2;
+    }
+    if (w == 0 && l == 0) {
+      dst[nn::OB2 + 0] = b2_0;
+      dst[nn::OB2 + 1] = b2_1;
+      dst[nn::OB2 + 2] = b2_2;
+    }
+  }
+}
+
+
+// AR chain launcher (chain_ar.hip): k_chain3<0, loss_log> on `s`, `blocks` workgroups.
+int launch_chain_ar(const ChainArgs& C, int blocks, bool loss_log, hipStream_t s);
+
+}  // namespace chain
+}  // namespace nfsp

@@ -156,6 +156,9 @@ __device__ inline void fwd_lds(const float* __restrict__ sw, uint32_t x, int act
     }
   }
   float o0 = 0.f, o1 = 0.f, o2 = 0.f;
+  // unrolled: the LDS reads of several hidden units go out together (the o sums keep their
+  // j order, so the result is unchanged)
+#pragma unroll 8
   for (int j = 0; j < nn::H; ++j) {
     float acc = 0.f;
 #pragma unroll

@@ -3,7 +3,9 @@
 // split of waves 0..3 (s_memtime).  Mode "compare" checks k_chain3 against the previous
 // f32-MFMA chain (tools/chain_ref.hip) from the same start.  Not part of libnfsp.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -mllvm -amdgpu-mfma-vgpr-form -fno-slp-vectorize \
-//         -Iinclude -I<pkg>/csrc tools/bench_chain.hip   (the flags of learner.hip in build())
+//         -fno-honor-nans -falign-loops=64 -mllvm -amdgpu-sched-strategy=max-ilp \
+//         [-mllvm -amdgpu-use-amdgpu-trackers] -Iinclude -I<pkg>/csrc tools/bench_chain.hip
+//   (one binary, one set of flags: build() gives the BR chain the trackers, the AR chain not)
 //   ./bench_chain <updates> <relu 0|1> [time|compare] [blocks 1|2] [layer-2 weight scale]
 #include <math.h>
 #include <stdio.h>
@@ -14,6 +16,7 @@
 #include <vector>
 
 #include "../neural-ficititious-self-play-in-imperfect-information-games_amd/csrc/learner.hip"
+#include "../neural-ficititious-self-play-in-imperfect-information-games_amd/csrc/chain_ar.hip"
 #include "chain_ref.hip"
 
 // the host helpers learner.hip's nfsp_engine_update references (unused here)
