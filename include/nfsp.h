@@ -212,6 +212,9 @@ int nfsp_engine_weights(nfsp_engine* e, int agent, int net, float** dev_w);
 int nfsp_rollout(nfsp_engine* e);
 int nfsp_engine_update(nfsp_engine* e);
 int nfsp_engine_step(nfsp_engine* e);          /* nfsp_rollout + nfsp_engine_update */
+/* After a non-OK return from nfsp_rollout / nfsp_engine_update / nfsp_engine_step the
+ * engine's state is unspecified: part of the step's work may have run.  Destroy the
+ * engine (nfsp_engine_destroy waits for all of its streams). */
 int nfsp_engine_get_stats(nfsp_engine* e, nfsp_engine_stats* out);   /* synchronises */
 /* Agent's memories in the reference's fp32 tuple layout (utils/replay_buffer.py:53-57),
  * expanded on the ctx stream at the call from the packed device records (M_RL: 32 B

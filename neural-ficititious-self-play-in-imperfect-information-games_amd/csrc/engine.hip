@@ -401,7 +401,11 @@ extern "C" int nfsp_engine_default_cfg(nfsp_engine_cfg* c) {
 
 extern "C" int nfsp_engine_destroy(nfsp_engine* e) {
   if (!e) return NFSP_OK;
+  // every stream the engine enqueues on: an update that failed midway may have left a chain
+  // running on a side stream without its join into the ctx stream
   if (e->ctx) (void)hipStreamSynchronize(e->ctx->stream);
+  for (hipStream_t st : {e->s_br[0], e->s_br[1], e->s_ar})
+    if (st) (void)hipStreamSynchronize(st);
   for (void* p : e->allocs) (void)hipFree(p);
   for (auto& m : e->marks) {
     e->pool.push_back(m.second.first);
@@ -586,12 +590,15 @@ extern "C" int nfsp_engine_memories(nfsp_engine* e, int agent, nfsp_records* rl,
                                     nfsp_records* sl, uint32_t** px, float** pa, int64_t** ppos) {
   NFSP_REQUIRE(e && (agent == 0 || agent == 1), "bad argument");
   Memories& M = e->M;
-  if ((rl || sl) && !M.ex_rl_s) {      // the fp32 reference-layout views, on first use
+  if ((rl || sl) && !M.ex_sl_a) {      // the fp32 reference-layout views, on first use
+    // (resumable: a failed allocation leaves the export unusable until a later call
+    // completes the set -- ex_sl_a, the last one, is the "all allocated" mark)
     const int64_t lc = 2 * M.log_cap, sc = 2 * M.sl_cap;
     for (auto pr : {std::make_pair((void**)&M.ex_rl_s, 4 * nfsp::OBS * lc), std::make_pair((void**)&M.ex_rl_s2, 4 * nfsp::OBS * lc),
                     std::make_pair((void**)&M.ex_rl_a, 4 * 3 * lc), std::make_pair((void**)&M.ex_rl_r, 4 * lc),
                     std::make_pair((void**)&M.ex_rl_t, lc), std::make_pair((void**)&M.ex_sl_s, 4 * nfsp::OBS * sc),
                     std::make_pair((void**)&M.ex_sl_a, 4 * 3 * sc)}) {
+      if (*pr.first) continue;
       NFSP_HIP(hipMalloc(pr.first, (size_t)pr.second));
       e->allocs.push_back(*pr.first);
     }
