@@ -2,6 +2,8 @@
 // instantiate it: learner.hip (BR, k_chain3<1, *>) and chain_ar.hip (AR, k_chain3<0, *>).
 // The two are compiled with different scheduler flags (__graft_entry__.FILE_FLAGS).
 #pragma once
+#include <atomic>
+
 #include "engine_internal.h"
 
 namespace nfsp {
@@ -485,6 +487,19 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
   }
 }
 
+
+// The chains' dynamic-LDS attribute (CHAIN_LDS), set once per device and kernel pair
+// (`mask`: one bit per device, kept by the caller's translation unit).
+inline int set_chain_lds(std::atomic<uint64_t>& mask, const void* f0, const void* f1) {
+  int dev = 0;
+  NFSP_HIP(hipGetDevice(&dev));
+  const uint64_t bit = 1ull << (dev & 63);
+  if (mask.load(std::memory_order_acquire) & bit) return NFSP_OK;
+  for (const void* f : {f0, f1})
+    NFSP_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, CHAIN_LDS));
+  mask.fetch_or(bit, std::memory_order_acq_rel);
+  return NFSP_OK;
+}
 
 // AR chain launcher (chain_ar.hip): k_chain3<0, loss_log> on `s`, `blocks` workgroups.
 int launch_chain_ar(const ChainArgs& C, int blocks, bool loss_log, hipStream_t s);

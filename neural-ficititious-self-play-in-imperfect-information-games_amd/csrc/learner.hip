@@ -457,11 +457,10 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
     NFSP_LAUNCHED("k_res_apply");
   }
   }
-  static bool attr = false;
-  if (!attr) {
-    for (const void* f : {(const void*)k_chain3<1, 0>, (const void*)k_chain3<1, 1>})   // AR: chain_ar.hip
-      NFSP_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, CHAIN_LDS));
-    attr = true;
+  {                                    // the BR chain's LDS attribute (AR: chain_ar.hip)
+    static std::atomic<uint64_t> attr{0};
+    const int rc = set_chain_lds(attr, (const void*)k_chain3<1, 0>, (const void*)k_chain3<1, 1>);
+    if (rc != NFSP_OK) return rc;
   }
   for (int a = 0; a < 2; ++a) {
     e->last_U[a] = P.A[a].U;
