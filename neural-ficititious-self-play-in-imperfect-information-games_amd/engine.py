@@ -74,7 +74,7 @@ class SelfPlayEngine:
 
     def weights_tensor(self, agent, net) -> torch.Tensor:
         """A torch view (no copy) of the device weights of (agent, net)."""
-        return _wrap_device(self._wptr(agent, net), NP, torch.float32, self.dev)
+        return _wrap_device(self._wptr(agent, net), NP, torch.float32, self.dev, self)
 
     def get_weights(self, agent, net) -> np.ndarray:
         return self.weights_tensor(agent, net).cpu().numpy().copy()
@@ -122,18 +122,18 @@ class SelfPlayEngine:
         d = self.dev
         out = dict(
             log_cap=n,
-            rl_s=_wrap_device(rl.s, n * 30, torch.float32, d).view(n, 30),
-            rl_a=_wrap_device(rl.a, n * 3, torch.float32, d).view(n, 3),
-            rl_r=_wrap_device(rl.r, n, torch.float32, d),
-            rl_s2=_wrap_device(rl.s2, n * 30, torch.float32, d).view(n, 30),
-            rl_t=_wrap_device(rl.t, n, torch.uint8, d),
-            sl_s=_wrap_device(sl.s, sl.cap * 30, torch.float32, d).view(sl.cap, 30),
-            sl_a=_wrap_device(sl.a, sl.cap * 3, torch.float32, d).view(sl.cap, 3),
+            rl_s=_wrap_device(rl.s, n * 30, torch.float32, d, self).view(n, 30),
+            rl_a=_wrap_device(rl.a, n * 3, torch.float32, d, self).view(n, 3),
+            rl_r=_wrap_device(rl.r, n, torch.float32, d, self),
+            rl_s2=_wrap_device(rl.s2, n * 30, torch.float32, d, self).view(n, 30),
+            rl_t=_wrap_device(rl.t, n, torch.uint8, d, self),
+            sl_s=_wrap_device(sl.s, sl.cap * 30, torch.float32, d, self).view(sl.cap, 30),
+            sl_a=_wrap_device(sl.a, sl.cap * 3, torch.float32, d, self).view(sl.cap, 3),
         )
         pc = 4 * self.cfg.n_lanes
-        out["pend_x"] = _wrap_device(px.value, pc, torch.int32, d)
-        out["pend_a"] = _wrap_device(pa.value, pc * 3, torch.float32, d).view(pc, 3)
-        out["pend_pos"] = _wrap_device(pp.value, pc, torch.int64, d)
+        out["pend_x"] = _wrap_device(px.value, pc, torch.int32, d, self)
+        out["pend_a"] = _wrap_device(pa.value, pc * 3, torch.float32, d, self).view(pc, 3)
+        out["pend_pos"] = _wrap_device(pp.value, pc, torch.int64, d, self)
         return out
 
     def last_update(self, agent, role):
@@ -186,14 +186,17 @@ def exploitability(ctx, dev_w_ar0: int, dev_w_ar1: int, mode: int = 0) -> dict:
     return {"br0": out[0], "br1": out[1], "exploitability": out[2], "value0": out[3]}
 
 
-def _wrap_device(addr, numel, dtype, device) -> torch.Tensor:
-    """Zero-copy torch view of device memory owned by libnfsp."""
+def _wrap_device(addr, numel, dtype, device, owner=None) -> torch.Tensor:
+    """Zero-copy torch view of device memory owned by libnfsp.  ``owner`` (the engine) is
+    referenced by the view's array-interface object, which torch keeps alive with the tensor:
+    the engine -- and so the memory -- outlives every view of it."""
     if numel == 0:
         return torch.empty(0, dtype=dtype, device=device)
 
     class _Holder:
         pass
     h = _Holder()
+    h.owner = owner
     esize = torch.empty(0, dtype=dtype).element_size()
     h.__cuda_array_interface__ = {
         "shape": (int(numel),), "typestr": torch.empty(0, dtype=dtype).numpy().dtype.str,

@@ -197,3 +197,22 @@ def test_engine_steps_are_deterministic(pkg):
     assert s1 == s2
     assert np.array_equal(w1, w2)
     assert s1["br_updates"][0] > 10 and s1["ar_updates"][0] > 0
+
+
+@pytest.mark.gpu
+def test_device_views_keep_the_engine_alive(pkg):
+    """Zero-copy views (weights, memories) reference the engine: its device memory outlives them."""
+    import gc
+    import weakref
+    eng = pkg.engine.SelfPlayEngine(n_lanes=256, rl_capacity=1000, sl_capacity=1000)
+    eng.step()
+    w = eng.weights_tensor(0, 0)
+    m = eng.memories(0)["rl_s"]
+    ref = weakref.ref(eng)
+    del eng
+    gc.collect()
+    assert ref() is not None
+    assert torch.isfinite(w).all() and m.shape[1] == 30
+    del w, m
+    gc.collect()
+    assert ref() is None
