@@ -437,26 +437,6 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
     maxUbr = pl.U_br > maxUbr ? pl.U_br : maxUbr;
     maxSL = pl.n_sl > maxSL ? pl.n_sl : maxSL;
   }
-  // ---- parallel prep on the ctx stream
-  {
-  KTimer kprep(e, KT_PREP);
-  if (maxUbr > 0) {
-    k_br_prep<<<dim3((unsigned)maxUbr, 2), 128, 0, s>>>(P);
-    NFSP_LAUNCHED("k_br_prep");
-  }
-  if (maxSL > 0) {
-    k_ar_slots<<<dim3(nfsp_blocks(maxSL, 256), 2), 256, 0, s>>>(P);
-    NFSP_LAUNCHED("k_ar_slots");
-  }
-  if (maxU > 0) {
-    k_ar_prep<<<dim3((unsigned)maxU, 2), 128, 0, s>>>(P);
-    NFSP_LAUNCHED("k_ar_prep");
-  }
-  if (maxSL > 0) {
-    k_res_apply<<<dim3(nfsp_blocks(maxSL, 256), 2), 256, 0, s>>>(P);
-    NFSP_LAUNCHED("k_res_apply");
-  }
-  }
   {                                    // the BR chain's LDS attribute (AR: chain_ar.hip)
     static std::atomic<uint64_t> attr{0};
     const int rc = set_chain_lds(attr, (const void*)k_chain3<1, 0>, (const void*)k_chain3<1, 1>);
@@ -465,15 +445,41 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
   for (int a = 0; a < 2; ++a) {
     e->last_U[a] = P.A[a].U;
     e->last_Ubr[a] = P.A[a].U_br;
-    if (e->log_loss) {       // NaN = no fit recorded (inactive AR update)
-      NFSP_HIP(hipMemsetAsync(e->LB.ar_loss + a * e->LB.umax * cfg.epochs, 0xFF,
-                              sizeof(float) * P.A[a].U * cfg.epochs, s));
+  }
+  // ---- parallel prep on the ctx stream, in the order the chains need it: the BR rows
+  // first (agent 0's BR segments are the learner's critical path), the BR streams fork;
+  // then the AR records, the AR stream forks; the final reservoir last (only the next
+  // rollout reads it, and it must follow k_ar_prep, which reads the reservoir as it was)
+  hipEvent_t fork_br = take_event(e), fork = take_event(e);
+  {
+  KTimer kprep(e, KT_PREP);
+  if (maxUbr > 0) {
+    k_br_prep<<<dim3((unsigned)maxUbr, 2), 128, 0, s>>>(P);
+    NFSP_LAUNCHED("k_br_prep");
+  }
+  if (e->log_loss)                     // NaN = no fit recorded
+    for (int a = 0; a < 2; ++a)
       NFSP_HIP(hipMemsetAsync(e->LB.br_loss + a * e->LB.umax * cfg.epochs, 0xFF,
                               sizeof(float) * P.A[a].U_br * cfg.epochs, s));
-    }
+  NFSP_HIP(hipEventRecord(fork_br, s));
+  if (maxSL > 0) {
+    k_ar_slots<<<dim3(nfsp_blocks(maxSL, 256), 2), 256, 0, s>>>(P);
+    NFSP_LAUNCHED("k_ar_slots");
   }
-  hipEvent_t fork = take_event(e);
+  if (maxU > 0) {
+    k_ar_prep<<<dim3((unsigned)maxU, 2), 128, 0, s>>>(P);
+    NFSP_LAUNCHED("k_ar_prep");
+  }
+  if (e->log_loss)                     // NaN = no fit recorded (inactive AR update)
+    for (int a = 0; a < 2; ++a)
+      NFSP_HIP(hipMemsetAsync(e->LB.ar_loss + a * e->LB.umax * cfg.epochs, 0xFF,
+                              sizeof(float) * P.A[a].U * cfg.epochs, s));
   NFSP_HIP(hipEventRecord(fork, s));
+  if (maxSL > 0) {
+    k_res_apply<<<dim3(nfsp_blocks(maxSL, 256), 2), 256, 0, s>>>(P);
+    NFSP_LAUNCHED("k_res_apply");
+  }
+  }
   // ---- AR chains (both agents, one launch) on their own stream
   if (maxU > 0) {
     NFSP_HIP(hipStreamWaitEvent(e->s_ar, fork, 0));
@@ -514,7 +520,7 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
     F.n_sl[a] = pl.n_sl;
     F.U_br[a] = pl.U_br;
     hipStream_t sa = e->s_br[a];
-    NFSP_HIP(hipStreamWaitEvent(sa, serial_ar ? ar_done : fork, 0));
+    NFSP_HIP(hipStreamWaitEvent(sa, serial_ar ? ar_done : fork_br, 0));
     int64_t it = h.iteration[a], tc = h.target_count[a], syncs = h.target_syncs[a];
     double eps = h.epsilon[a];
     const int64_t it0 = it;
@@ -578,6 +584,7 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
     e->pool.push_back(j);      // reusable once the wait is enqueued
   }
   e->pool.push_back(fork);
+  e->pool.push_back(fork_br);
   if (ar_done != fork) e->pool.push_back(ar_done);
   k_finalize<<<1, 64, 0, s>>>(F);
   NFSP_LAUNCHED("k_finalize");
