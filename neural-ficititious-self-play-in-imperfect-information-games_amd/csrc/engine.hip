@@ -60,6 +60,7 @@ __global__ void __launch_bounds__(256) k_rollout(RolloutArgs A) {
     else d = LB1 + (q - nn::OB1);
     sw[net * NET_LDS + d] = v;
   }
+  for (int e = tid; e < 4 * nn::H; e += blockDim.x) sw[(e / nn::H) * NET_LDS + ZROW + e % nn::H] = 0.f;
   if (tid < 6) s_act[tid / 3][tid % 3] = 0;
   if (tid < 2) s_rew[tid] = 0;
   __syncthreads();

@@ -14,8 +14,9 @@ namespace eng {
 constexpr int MAXREC = 6;          // records of one kind per lane per hand (<= 6 decisions)
 constexpr int W1S = 65;            // padded LDS row stride of W1 for per-lane row gathers:
                                    // rows i, i' of two lanes hit banks (i + j), (i' + j) mod 32
-constexpr int NET_LDS = OBS * W1S + nn::H + nn::H * NA + NA;   // 2,209 floats
 constexpr int LB1 = OBS * W1S, LW2 = LB1 + nn::H, LB2 = LW2 + nn::H * NA;
+constexpr int ZROW = LB2 + NA;     // a row of +0.0: fwd_lds' unused gather slots point here
+constexpr int NET_LDS = ZROW + nn::H;                          // 2,273 floats
 constexpr int MAX_BATCH = 128;     // learner minibatch (config MiniBatchSize)
 constexpr int CHAIN_MB = 32;       // fit minibatch of the SGD chains (Keras batch_size)
 
@@ -137,23 +138,22 @@ __device__ inline void stage_net_lds(float* sw, const float* __restrict__ w, int
     const int d = q < nn::OB1 ? (q / nn::H) * W1S + (q % nn::H) : LB1 + (q - nn::OB1);
     sw[d] = w[q];
   }
+  for (int j = tid; j < nn::H; j += nt) sw[ZROW + j] = 0.f;
 }
 
 // Forward of one 0/1 observation (bits) through a net staged by stage_net_lds.  Same
 // operation order as oracle/nn_oracle.py (bit-exact for the ReLU head).
 __device__ inline void fwd_lds(const float* __restrict__ sw, uint32_t x, int act, float y[3]) {
 #pragma clang fp contract(off)
+  // the set bits' W1 rows in ascending order; the unused slots point at the zero row, so
+  // every hidden unit adds 9 terms without a branch.  Exact: acc starts at +0 and only
+  // gains finite values, so it is never -0, and a trailing + 0.0 leaves it unchanged.
   int rows[9];
-  int nb = 0;
   uint32_t b = x;
 #pragma unroll
   for (int u = 0; u < 9; ++u) {
-    rows[u] = 0;
-    if (b) {
-      rows[u] = __builtin_ctz(b) * W1S;
-      b &= b - 1;
-      nb = u + 1;
-    }
+    rows[u] = b ? __builtin_ctz(b) * W1S : ZROW;
+    b &= b - 1;
   }
   float o0 = 0.f, o1 = 0.f, o2 = 0.f;
   // unrolled: the LDS reads of several hidden units go out together (the o sums keep their
@@ -162,8 +162,7 @@ __device__ inline void fwd_lds(const float* __restrict__ sw, uint32_t x, int act
   for (int j = 0; j < nn::H; ++j) {
     float acc = 0.f;
 #pragma unroll
-    for (int u = 0; u < 9; ++u)
-      if (u < nb) acc = acc + sw[rows[u] + j];
+    for (int u = 0; u < 9; ++u) acc = acc + sw[rows[u] + j];
     if (b) {   // > 9 set bits: impossible for Leduc observations, kept exact anyway
       uint32_t rest = b;
       while (rest) {

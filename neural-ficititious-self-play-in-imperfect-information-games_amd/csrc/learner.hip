@@ -187,7 +187,6 @@ __global__ void __launch_bounds__(128) k_ar_prep(PrepArgs P) {
   __shared__ float ra[MAX_BATCH][3];
   __shared__ uint32_t px[MAX_BATCH];
   __shared__ float pt[MAX_BATCH][3];
-  __shared__ int64_t s_nb;
   const int a = blockIdx.y;
   const int64_t u = blockIdx.x;
   const AgentPlan& pl = P.A[a];
@@ -197,17 +196,21 @@ __global__ void __launch_bounds__(128) k_ar_prep(PrepArgs P) {
   const int64_t m = pl.m_first + u;
   const int64_t pm = m * P.c;
   const int64_t slot_u = (int64_t)a * P.LB.umax + u;
-  if (b == 0) {          // SL inserts made before the trigger: pend_pos is nondecreasing
-    const int64_t* pos = P.M.pend_pos + (int64_t)a * P.M.pend_cap;
-    int64_t lo = 0, hi = pl.n_sl;
-    while (lo < hi) {
-      const int64_t mid = (lo + hi) >> 1;
-      if (pos[mid] <= pm) lo = mid + 1; else hi = mid;
-    }
-    s_nb = lo;
+  // SL inserts made before the trigger (pend_pos is nondecreasing): a 128-ary search, a few
+  // rounds of one probe per thread instead of one thread's ~20 dependent loads.  lo / hi
+  // are block-uniform: every thread takes the same rounds.
+  const int64_t* pos = P.M.pend_pos + (int64_t)a * P.M.pend_cap;
+  const int nt = blockDim.x;
+  int64_t lo = 0, hi = pl.n_sl;
+  while (hi - lo > nt) {
+    const int64_t span = hi - lo;       // probe t at lo + span (t + 1) / (nt + 1): increasing
+    const int k = __syncthreads_count(pos[lo + span * (b + 1) / (nt + 1)] <= pm);
+    const int64_t below = lo + span * k / (nt + 1);          // probe k - 1 (k >= 1)
+    const int64_t above = lo + span * (k + 1) / (nt + 1);    // probe k (k < nt)
+    lo = k > 0 ? below + 1 : lo;
+    hi = k < nt ? above : hi;
   }
-  __syncthreads();
-  const int64_t nb = s_nb;
+  const int64_t nb = lo + __syncthreads_count(lo + b < hi && pos[lo + b] <= pm);
   const int64_t tot = pl.sl_total0 + nb;
   const int64_t count = tot < P.M.sl_cap ? tot : P.M.sl_cap;
   if (count <= P.B) {                         // size() > minibatch_size fails
