@@ -12,9 +12,11 @@ Workload (config.workload): C3 = 1,048,576 lanes per GPU, M_RL 200k, M_SL 2M, ta
 sync every 150 BR updates (BASELINE.json configs[2]; configs[3] is the same per GPU at
 N = 8).  `--config c2` selects configs[1] (65,536 lanes).
 
-Multi-GPU (`torch.distributed.run --nproc-per-node N bench.py --gpus N`): independent
-self-play replicas, one per GPU, seeds 1234 + rank, no data-path collective (weak
-scaling); a barrier and a max-over-ranks of the elapsed time bracket the timed region.
+Multi-GPU (`torch.distributed.run --nproc-per-node N bench.py --gpus N`, configs[3] = C4):
+one self-play shard per GPU (its own hands, memories and learner; seeds 1234 + rank; weak
+scaling), and once per engine step an RCCL all-reduce of the average-policy (AR) gradient
+steps of both agents (shards.AvgPolicyAllReduce, 17.4 KB; `--ar-allreduce off` = independent
+replicas).  A barrier and a max-over-ranks of the elapsed time bracket the timed region.
 
 Roofline: HIP events recorded on the engine's stream around every kernel launch give
 each kernel's average duration; the dominant kernel's algorithmic FLOPs (or bytes) per
@@ -182,6 +184,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL (one rank per GPU); gloo: a CPU-side rehearsal of the N > 1 path")
+    ap.add_argument("--ar-allreduce", default="auto", choices=["auto", "on", "off"],
+                    help="all-reduce of the AR (average-policy) gradient steps once per engine "
+                         "step over the ranks (C4; shards.AvgPolicyAllReduce); auto = on for N > 1")
     args = ap.parse_args()
 
     import torch
@@ -196,13 +201,24 @@ def main():
     eng = pkg.engine.SelfPlayEngine(n_lanes=cfg["n_lanes"], rl_capacity=cfg["rl_capacity"],
                                     sl_capacity=cfg["sl_capacity"], seed=1234 + rank,
                                     init_seed=rank, game=game)
-    for _ in range(args.warmup):
+    avg = None
+    if dist is not None and (args.ar_allreduce == "on" or (args.ar_allreduce == "auto" and world > 1)):
+        # C4: the AR nets of both agents, averaged over the ranks once per engine step
+        avg = pkg.shards.AvgPolicyAllReduce(
+            [eng.weights_tensor(a, pkg.engine.NET_AR) for a in (0, 1)], dist,
+            sync=torch.cuda.synchronize)
+
+    def step():
         eng.step()
+        if avg is not None:
+            avg()
+    for _ in range(args.warmup):
+        step()
     torch.cuda.synchronize()
     s0 = eng.stats()
     eng.set_timing(True)
     eng.timings()
-    elapsed = timed_steps(eng.step, args.steps, 0, dist, torch.cuda.synchronize,
+    elapsed = timed_steps(step, args.steps, 0, dist, torch.cuda.synchronize,
                           device="cuda" if args.dist_backend == "nccl" else "cpu")
     timings = eng.timings()
     s1 = eng.stats()
@@ -268,7 +284,8 @@ def main():
         "data": "synthetic: Philox self-play deals/draws, Glorot-uniform random-init nets",
         "config": {"workload": cfg["label"], "lanes_per_gpu": cfg["n_lanes"],
                    "rl_capacity": cfg["rl_capacity"], "sl_capacity": cfg["sl_capacity"],
-                   "inserts_per_update": 128, "batch": 128, "parallelism": f"replicas x{world}"},
+                   "inserts_per_update": 128, "batch": 128, "parallelism": (f"dp{world}: shards + AR-gradient all-reduce per engine step"
+                                   if avg is not None else f"replicas x{world}")},
         "roofline": roofline,
         "roofline_other": {k: v for k, v in roofs.items() if k != roofline["kernel"]},   # incl. the
         # dominant chain's HBM framing (k_chain3_br_hbm: SURVEY 8(d) bytes, PMC traffic)
@@ -278,6 +295,9 @@ def main():
                      "rl_inserts_per_hand": t_rl, "sl_inserts_per_hand": t_sl},
         "exploitability_proxy": sum(s1["exploitability"]),
     }
+    if avg is not None:
+        out["ar_allreduce"] = {"calls": avg.calls, "bytes_per_call": 4 * avg.flat.numel(),
+                               "backend": args.dist_backend, "per": "engine step"}
     # exact exploitability of the AR nets after the timed steps (outside the timed region)
     ex = {m: eng.exploitability(m) for m in (0, 1)}
     out["exploitability_exact"] = {
