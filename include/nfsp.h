@@ -247,6 +247,11 @@ int nfsp_engine_get_timings(nfsp_engine* e, double* ms /*[8]*/, int64_t* launche
  * rows [batch] (int64) and fit permutations [epochs][batch] (int32) of its LAST update. */
 int nfsp_engine_last_update(nfsp_engine* e, int agent, int role, int64_t** dev_rows,
                             int32_t** dev_perms);
+/* Debug view of the last rollout's per-lane record counts [n_lanes] (uint32, device):
+ * rl0 | rl1 << 4 | sl0 << 8 | sl1 << 12 (RL / SL inserts of agents 0 and 1 by that lane's
+ * hand).  Their exclusive prefix over lanes is each lane's first record in the canonical
+ * insert order (lane, then play order) -- how a test finds one lane's records in M_RL. */
+int nfsp_engine_lane_counts(nfsp_engine* e, uint32_t** dev_counts);
 
 /* ---- evaluation ----
  * Exact exploitability of two average-policy nets (packed weights, device pointers; e.g.

@@ -644,6 +644,12 @@ extern "C" int nfsp_engine_last_update(nfsp_engine* e, int agent, int role, int6
   return NFSP_OK;
 }
 
+extern "C" int nfsp_engine_lane_counts(nfsp_engine* e, uint32_t** counts) {
+  NFSP_REQUIRE(e && counts, "null argument");
+  *counts = e->S.counts;
+  return NFSP_OK;
+}
+
 extern "C" int nfsp_engine_set_timing(nfsp_engine* e, int on) {
   NFSP_REQUIRE(e, "null argument");
   e->timing = on != 0;

@@ -144,6 +144,16 @@ class SelfPlayEngine:
         return (_wrap_device(rows.value, B, torch.int64, self.dev).cpu().numpy(),
                 _wrap_device(perms.value, E * B, torch.int32, self.dev).view(E, B).cpu().numpy())
 
+    def lane_counts(self) -> np.ndarray:
+        """[n_lanes, 4] (RL agent 0, RL agent 1, SL agent 0, SL agent 1) records of each lane's
+        hand in the last rollout (nfsp_engine_lane_counts; synchronises)."""
+        p = native.P()
+        native.check(self.L.nfsp_engine_lane_counts(self.h, C.byref(p)), "lane_counts")
+        torch.cuda.synchronize(self.dev)
+        c = _wrap_device(p.value, self.cfg.n_lanes, torch.int32, self.dev).cpu().numpy()
+        c = c.astype(np.int64) & 0xFFFF
+        return np.stack([(c >> (4 * k)) & 15 for k in range(4)], axis=1)
+
     loss_log = False
 
     def set_loss_log(self, on=True):
