@@ -91,3 +91,48 @@ def test_learner_step_matches_oracle(pkg, case, quirks):
         size = int(st1["sl_size"][a])
         assert np.array_equal(_bits(m["sl_s"].cpu().numpy()[:size]), W["res_x"][:size])
         assert np.array_equal(m["sl_a"].cpu().numpy()[:size], W["res_a"][:size])
+
+
+@pytest.mark.gpu
+def test_single_lane_engine_matches_oracle(pkg):
+    """The reference's own configuration (C1: one env, one hand per step) through the engine:
+    every learner call that triggers updates is replayed by the oracle, with memories small
+    enough that M_RL wraps and the reservoir replaces within the run."""
+    eng = pkg.engine.SelfPlayEngine(n_lanes=1, rl_capacity=300, sl_capacity=150, target_every=3,
+                                    eta=0.5, seed=31337, init_seed=5)
+    c = eng.cfg
+    cfg = dict(c=c.inserts_per_update, batch=c.batch, epochs=c.epochs, rl_capacity=c.rl_capacity,
+               sl_capacity=c.sl_capacity, target_every=c.target_every, lr_br=c.lr_br, lr_ar=c.lr_ar,
+               gamma=c.gamma, seed=c.seed)
+    checked = ar_checked = 0
+    for _ in range(4000):
+        eng.rollout()
+        st = eng.stats()
+        due = any(st["rl_total"][a] // c.inserts_per_update > (st["rl_total"][a] - st["last_rl"][a]) // c.inserts_per_update
+                  for a in (0, 1))
+        if not due:
+            eng.update()
+            continue
+        st0, state = _snapshot(eng)
+        eng.update()
+        st1 = eng.stats()
+        want = LO.learner_step(cfg, state, quirks=c.quirks)
+        for a in (0, 1):
+            W = want[a]
+            assert st1["br_updates"][a] == W["br_updates"]
+            assert st1["ar_updates"][a] - st0["ar_updates"][a] == W["ar_updates"]
+            assert st1["iteration"][a] == W["iteration"]
+            assert st1["epsilon"][a] == pytest.approx(W["epsilon"], rel=1e-12)
+            ar_checked += W["ar_updates"]
+            for n in (0, 1, 2):
+                d = np.abs(eng.get_weights(a, n) - W["w"][n])
+                assert d.max() <= 1e-4, (a, n, d.max())
+            size = int(st1["sl_size"][a])
+            m = eng.memories(a)
+            assert np.array_equal(_bits(m["sl_s"].cpu().numpy()[:size]), W["res_x"][:size])
+        checked += 1
+        if (checked >= 12 and ar_checked >= 4 and min(st1["rl_total"]) > c.rl_capacity
+                and max(st1["sl_total"]) > c.sl_capacity):
+            break
+    assert checked >= 12 and ar_checked >= 4
+    assert min(st1["rl_total"]) > c.rl_capacity and max(st1["sl_total"]) > c.sl_capacity
