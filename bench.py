@@ -51,8 +51,9 @@ CONFIGS = {
                label="C2: 65,536 Leduc lanes/GPU, M_RL/M_SL 40k, eta 0.1, 2x64 MLP heads, "
                      "reference update cadence"),
     "c3_4k": dict(n_lanes=4_096, rl_capacity=200_000, sl_capacity=2_000_000,
-                  label="C3's memories and cadence at 4,096 lanes: the operating point whose "
-                        "exploitability curve stays in the CPU reference's seed band (DESIGN §9)"),
+                  label="C3's memories and cadence at 4,096 lanes (policy lag 4k hands; DESIGN §9)"),
+    "c3_64k": dict(n_lanes=65_536, rl_capacity=200_000, sl_capacity=2_000_000,
+                   label="C3's memories and cadence at 65,536 lanes (policy lag 64k hands; DESIGN §9)"),
     "c5": dict(n_lanes=1_048_576, rl_capacity=200_000, sl_capacity=2_000_000, game="kuhn",
                label="C5: Kuhn swap-in, 1,048,576 lanes/GPU, C3's memories and cadence"),
 }
