@@ -60,6 +60,7 @@ CONFIGS = {
 
 PEAK_FP32_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA peak
 PEAK_HBM_GBS = 8000.0         # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
+CHAIN_CLOCK_HZ = 2.40e9       # the chains' effective shader clock (tools/chain_clock.py)
 # algorithmic work per unit (DESIGN.md "Measurement")
 F_FWD = 2 * (30 * 64 + 64 * 3)          # 4,224 FLOP per row forward (dense-equivalent)
 F_TRAIN = 3 * F_FWD                      # forward + backward (dX, dW) per row
@@ -260,10 +261,31 @@ def main():
         return {"kernel": name, "bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS,
                 "unit": "GB/s", "frac": ach / PEAK_HBM_GBS, "traffic": load_pmc(args.config, name),
                 "avg_ms": k_ms[name], "launches": k_launches[name], "bytes_per_launch": byt}
+    def chain_issue(name, updates, net):
+        """The chain's step as an issue roofline: the loop's static issue cycles per SGD step
+        (tools/chain_census.py -> profiles/r01_chain_census.json, MI355X_MICROARCH.md issue
+        costs) against the measured cycles per step at the chain's effective clock (2.40 GHz,
+        tools/chain_clock.py).  frac = the share of the step one wave spends issuing."""
+        path = os.path.join(REPO, "profiles", "r01_chain_census.json")
+        n = max(k_launches[name], 1)
+        steps = updates * 2 * 128 / 32 / n                  # epochs x minibatches per launch
+        if not os.path.exists(path) or steps <= 0:
+            return None
+        with open(path) as f:
+            issue = json.load(f)[net]["issue_cycles_per_step"]
+        measured = k_ms[name] * 1e-3 / steps * CHAIN_CLOCK_HZ
+        return {"kernel": name, "bound": "issue", "achieved": issue, "peak": measured,
+                "unit": "cycles per SGD step (static issue / measured)", "frac": issue / measured,
+                "us_per_step": k_ms[name] * 1e3 / steps, "source": "profiles/r01_chain_census.json"}
     roofs = {"k_chain3_br": chain_roof("k_chain3_br", br_upd),
              "k_chain3_ar": chain_roof("k_chain3_ar", ar_upd),
              "k_rollout": roof_rollout,
-             "k_chain3_br_hbm": chain_roof_hbm("k_chain3_br", br_upd, BYTES_RL)}
+             "k_chain3_br_hbm": chain_roof_hbm("k_chain3_br", br_upd, BYTES_RL),
+             "k_chain3_br_issue": chain_issue("k_chain3_br", br_upd, "br"),
+             # one AR launch runs both agents' chains side by side: it lasts as long as the
+             # agent with more updates
+             "k_chain3_ar_issue": chain_issue("k_chain3_ar", max(s1["ar_updates"][a] - s0["ar_updates"][a]
+                                                                 for a in (0, 1)), "ar")}
     # the dominant kernel = largest GPU time inside the timed region
     singles = [k for k in timings if k != "learner"]
     dom = max(singles, key=lambda k: timings[k][0])

@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""Instruction census of the SGD chain's step loop (k_chain3), from the gfx950 assembly of
+the two translation units as __graft_entry__ builds them (learner.hip: BR, chain_ar.hip: AR).
+
+For each chain it counts the instructions of the loop body (one SGD step) by class and
+prices their issue with the per-instruction constants of MI355X_MICROARCH.md ('vector-
+instruction ISSUE cost, one wave's stream on one SIMD'): VALU 4 cycles, transcendental
+(v_exp / v_log / v_rcp / v_rsq / v_sqrt) 8, v_mfma_f32_16x16x32_bf16 8 (it holds the SIMD's
+vector issue for 8 of its 16 cycles), s_nop 4; LDS / VMEM / SALU / waitcnt / branch 1.
+bench.py divides that issue estimate by the measured cycles per step: the fraction of a
+step one wave spends issuing (the chain is one wave per SIMD, so nothing else fills it).
+
+    python tools/chain_census.py > profiles/r01_chain_census.json
+"""
+import collections
+import json
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+KERNELS = {"br": ("learner.hip", "_ZN4nfsp5chain8k_chain3ILi1ELi0E"),
+           "ar": ("chain_ar.hip", "_ZN4nfsp5chain8k_chain3ILi0ELi0E")}
+TRANS = ("v_exp_f32", "v_log_f32", "v_rcp_f32", "v_rsq_f32", "v_sqrt_f32")
+
+
+def asm(src):
+    import __graft_entry__ as g
+    out = os.path.join(tempfile.mkdtemp(), os.path.basename(src) + ".s")
+    subprocess.check_call([g.HIPCC, *g.HIPFLAGS, *g.FILE_FLAGS.get(src, []), "--cuda-device-only", "-S",
+                           os.path.join(g.CSRC, src), "-o", out], stderr=subprocess.DEVNULL)
+    return open(out).read().split("\n")
+
+
+def loop_body(lines, kernel):
+    start = next(i for i, l in enumerate(lines) if l.startswith(kernel))
+    best = None
+    for h in [i for i in range(start, len(lines)) if "Loop Header" in lines[i]][:8]:
+        lab = lines[h].split(":")[0]
+        end = next((i for i in range(h, min(len(lines), h + 4000))
+                    if re.search(r"s_cbranch_\w+\s+" + re.escape(lab) + r"\s*$", lines[i])), None)
+        if end is None:
+            continue
+        body = [l.strip() for l in lines[h + 1:end + 1]
+                if l.strip() and not l.strip().startswith((";", "."))]
+        if best is None or len(body) > len(best):
+            best = body
+    return best
+
+
+def price(op):
+    if op.startswith("v_mfma"):
+        return "mfma", 8
+    if op.startswith(TRANS):
+        return "trans", 8
+    if op.startswith("v_"):
+        return "valu", 4
+    if op == "s_nop":
+        return "nop", 4
+    if op.startswith("ds_"):
+        return "lds", 1
+    if op.startswith(("global_", "buffer_")):
+        return "vmem", 1
+    return "salu/other", 1
+
+
+def main():
+    out = {"source": "tools/chain_census.py (gfx950 assembly with the build's flags)",
+           "prices": "MI355X_MICROARCH.md issue costs: VALU 4, transcendental 8, MFMA 16x16x32 8, "
+                     "s_nop 4, other 1 cycle"}
+    for name, (src, kern) in KERNELS.items():
+        body = loop_body(asm(src), kern)
+        ops = collections.Counter(l.split()[0] for l in body)
+        cls = collections.Counter()
+        cyc = collections.Counter()
+        for op, n in ops.items():
+            k, c = price(op)
+            cls[k] += n
+            cyc[k] += n * c
+        out[name] = {"instructions": len(body), "by_class": dict(cls), "issue_cycles": dict(cyc),
+                     "issue_cycles_per_step": sum(cyc.values())}
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
