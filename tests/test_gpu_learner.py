@@ -28,6 +28,9 @@ CASES = {
     "leduc": (CFG, "leduc"),
     "tiny_memories": (dict(n_lanes=1024, rl_capacity=200, sl_capacity=150, target_every=7, seed=99), "leduc"),
     "kuhn": (dict(n_lanes=4096, rl_capacity=3000, sl_capacity=2000, target_every=10, seed=7), "kuhn"),
+    # the cfg's other fit shapes: minibatch sample of 64 rows, 3 epochs, an update every 96 inserts
+    "batch64_e3": (dict(n_lanes=4096, rl_capacity=3000, sl_capacity=2000, target_every=20, seed=11,
+                        batch=64, epochs=3, inserts_per_update=96), "leduc"),
 }
 
 
@@ -57,7 +60,8 @@ def _snapshot(eng):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case,quirks", [("leduc", 7), ("leduc", 0), ("tiny_memories", 7), ("kuhn", 7)])
+@pytest.mark.parametrize("case,quirks", [("leduc", 7), ("leduc", 0), ("tiny_memories", 7), ("kuhn", 7),
+                                         ("batch64_e3", 7)])
 def test_learner_step_matches_oracle(pkg, case, quirks):
     cfg_e, game = CASES[case]
     g = pkg.native.GAME_KUHN if game == "kuhn" else pkg.native.GAME_LEDUC
