@@ -111,6 +111,16 @@ int nfsp_env_get_state(nfsp_ctx* ctx, int p, const uint8_t* dev_players,
  * untouched (dev_mask may be NULL = all). */
 int nfsp_env_step(nfsp_ctx* ctx, const float* dev_action /*[n,3]*/, int p,
                   const uint8_t* dev_players, const uint8_t* dev_mask);
+/* Env.do_action(action, p) (leduc/newenv.py:131-178) alone: argmax, last_action, the
+ * illegal-raise remap, then the action recorded (history, pot, actions_done; a fold too).
+ * No round change, termination or reward (those are step()'s).  dev_fold[i] = its return
+ * value (1 on a fold); dev_fold may be NULL. */
+int nfsp_env_do_action(nfsp_ctx* ctx, const float* dev_action /*[n,3]*/, int p,
+                       const uint8_t* dev_players, const uint8_t* dev_mask, uint8_t* dev_fold /*[n]*/);
+/* Env.game_or_round_has_terminated() (leduc/newenv.py:180-190) on each env's actions_done:
+ * 1 = True ([C,C] [R,C] [C,R,C] [R,R,C]), 0 = False (length other than 2 or 3),
+ * -1 = None (the reference's fall-through for other length-2 / -3 sequences). */
+int nfsp_env_round_status(nfsp_ctx* ctx, int8_t* dev_out /*[n]*/);
 /* Env.round_index (leduc/newenv.py:59-61) */
 int nfsp_env_round(nfsp_ctx* ctx, uint8_t* dev_round /*[n]*/);
 /* Debug/introspection: the 64-byte per-env state (layout nfsp_device.h `Hand`). */

@@ -83,6 +83,24 @@ __global__ void k_env_step(Hand* __restrict__ hands, int n, const float* __restr
   hands[i] = h;
 }
 
+__global__ void k_env_do_action(Hand* __restrict__ hands, int n, const float* __restrict__ action, int p,
+                                const uint8_t* __restrict__ players, const uint8_t* __restrict__ mask,
+                                uint8_t* __restrict__ fold) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (mask && !mask[i]) return;
+  Hand h = hands[i];
+  const int q = players ? (players[i] & 1) : p;
+  const bool f = nfsp::hand_do_action(h, q, action[3 * i], action[3 * i + 1], action[3 * i + 2]);
+  hands[i] = h;
+  if (fold) fold[i] = f ? 1 : 0;
+}
+
+__global__ void k_env_round_status(const Hand* __restrict__ hands, int n, int8_t* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (int8_t)nfsp::hand_round_status(hands[i]);
+}
+
 __global__ void k_env_round(const Hand* __restrict__ hands, int n, uint8_t* __restrict__ out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = hands[i].rnd;
@@ -178,6 +196,23 @@ extern "C" int nfsp_env_step(nfsp_ctx* c, const float* action, int p, const uint
   k_env_step<<<nfsp_blocks(c->n_envs, 256), 256, 0, c->stream>>>(c->hands, c->n_envs, action,
                                                                   p & 1, players, mask);
   NFSP_LAUNCHED("k_env_step");
+  return NFSP_OK;
+}
+
+extern "C" int nfsp_env_do_action(nfsp_ctx* c, const float* action, int p, const uint8_t* players,
+                                  const uint8_t* mask, uint8_t* fold) {
+  NFSP_REQUIRE(c && action, "null argument");
+  NFSP_REQUIRE(p == 0 || p == 1 || players, "player must be 0 or 1");
+  k_env_do_action<<<nfsp_blocks(c->n_envs, 256), 256, 0, c->stream>>>(c->hands, c->n_envs, action,
+                                                                       p & 1, players, mask, fold);
+  NFSP_LAUNCHED("k_env_do_action");
+  return NFSP_OK;
+}
+
+extern "C" int nfsp_env_round_status(nfsp_ctx* c, int8_t* out) {
+  NFSP_REQUIRE(c && out, "null argument");
+  k_env_round_status<<<nfsp_blocks(c->n_envs, 256), 256, 0, c->stream>>>(c->hands, c->n_envs, out);
+  NFSP_LAUNCHED("k_env_round_status");
   return NFSP_OK;
 }
 

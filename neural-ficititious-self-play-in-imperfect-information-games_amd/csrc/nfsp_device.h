@@ -146,19 +146,16 @@ __host__ __device__ inline bool hand_raise_legal(const Hand& h, int p) {
   return !((p ? h.raises1 : h.raises0) > 0 || (h.ndone == 2 && h.done0 == A_CALL && h.done1 == A_RAISE));
 }
 
-// env.step(action, p).  Returns nothing; mirrors every side effect of the reference.
-__host__ __device__ inline void hand_step(Hand& h, int p, float a0, float a1, float a2) {
-  h.s[p] = hand_obs(h, p);                      // newenv.py:200-202, even after the end
-  if (h.term) { h.warn++; return; }             // newenv.py:346-348
-  const int o = 1 - p;
-  const int raw = argmax3(a0, a1, a2);
-  int v = raw;
+// Env.do_action(action, p) (leduc/newenv.py:131-178): argmax (first max wins), store
+// last_action, remap an illegal raise to a call, then record the action.  A fold is recorded
+// too (actions_done.append('Fold')) and returns true; termination and round changes are
+// step()'s.
+__host__ __device__ inline bool hand_do_action(Hand& h, int p, float a0, float a1, float a2) {
+  int v = argmax3(a0, a1, a2);
   h.la[p][0] = a0; h.la[p][1] = a1; h.la[p][2] = a2;
   const bool kuhn = h.game == GAME_KUHN;
   if (v == A_RAISE && !hand_raise_legal(h, p)) v = A_CALL;
-  if (v == A_FOLD) {
-    h.term = 1;
-  } else {
+  if (v != A_FOLD) {
     const bool prev_raise = h.ndone > 0 &&
         (h.ndone == 1 ? h.done0 : (h.ndone == 2 ? h.done1 : h.done2)) == A_RAISE;
     const bool opener = h.rnd == 0 && h.ndone == 0;
@@ -172,22 +169,42 @@ __host__ __device__ inline void hand_step(Hand& h, int p, float a0, float a1, fl
       c += prev_raise ? 4 : 2;
     }
     if (opener && !kuhn) c += 1;                 // the dealer completes its blind
-    if (h.ndone == 0) h.done0 = (uint8_t)v;
-    else if (h.ndone == 1) h.done1 = (uint8_t)v;
-    else h.done2 = (uint8_t)v;
-    h.ndone++;
-    const bool over =
-        (h.ndone == 2 && h.done1 == A_CALL) ||                        // [C,C] [R,C]
-        (h.ndone == 3 && h.done1 == A_RAISE && h.done2 == A_CALL);    // [C,R,C] [R,R,C]
-    if (over) {
-      if (h.rnd == 1 || kuhn) {
-        h.term = 1;
-      } else {
-        h.rnd = 1;
-        h.raises0 = h.raises1 = 0;
-        h.slot = 0;
-        h.ndone = 0;
-      }
+  }
+  if (h.ndone == 0) h.done0 = (uint8_t)v;        // a round holds at most 3 actions
+  else if (h.ndone == 1) h.done1 = (uint8_t)v;
+  else h.done2 = (uint8_t)v;
+  h.ndone++;
+  return v == A_FOLD;
+}
+
+// Env.game_or_round_has_terminated() (leduc/newenv.py:180-190) on actions_done:
+// 1 = True ([C,C] [R,C] [C,R,C] [R,R,C]), 0 = False (length other than 2 or 3),
+// -1 = None (a length-2 or -3 sequence that does not end the round).
+__host__ __device__ inline int hand_round_status(const Hand& h) {
+  if (h.ndone == 2)
+    return ((h.done0 == A_CALL || h.done0 == A_RAISE) && h.done1 == A_CALL) ? 1 : -1;
+  if (h.ndone == 3)
+    return ((h.done0 == A_CALL || h.done0 == A_RAISE) && h.done1 == A_RAISE && h.done2 == A_CALL) ? 1 : -1;
+  return 0;
+}
+
+// env.step(action, p).  Returns nothing; mirrors every side effect of the reference.
+__host__ __device__ inline void hand_step(Hand& h, int p, float a0, float a1, float a2) {
+  h.s[p] = hand_obs(h, p);                      // newenv.py:200-202, even after the end
+  if (h.term) { h.warn++; return; }             // newenv.py:346-348
+  const int o = 1 - p;
+  const int raw = argmax3(a0, a1, a2);
+  const bool kuhn = h.game == GAME_KUHN;
+  if (hand_do_action(h, p, a0, a1, a2)) {
+    h.term = 1;
+  } else if (hand_round_status(h) == 1) {
+    if (h.rnd == 1 || kuhn) {
+      h.term = 1;
+    } else {
+      h.rnd = 1;
+      h.raises0 = h.raises1 = 0;
+      h.slot = 0;
+      h.ndone = 0;
     }
   }
   if (h.term) {

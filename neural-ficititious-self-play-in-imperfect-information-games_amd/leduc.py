@@ -121,6 +121,24 @@ class Env:
 
     get_new_state = get_state
 
+    def do_action(self, action, p_index):
+        """Env.do_action (leduc/newenv.py:131-178) alone, on the device: records the action
+        (argmax, illegal raise -> call) without ending the round or the hand; True on a fold."""
+        p = int(p_index)
+        a = np.asarray(action, dtype=np.float32).reshape(3)
+        self._act.copy_(torch.from_numpy(a))
+        self.ctx.call("nfsp_env_do_action", native.ptr(self._act), p, None, None, native.ptr(self._t))
+        fold = bool(self._t.item())
+        self.last_action[p] = a
+        return fold
+
+    def game_or_round_has_terminated(self):
+        """leduc/newenv.py:180-190 on the device's actions_done: True, False, or the
+        reference's None for a length-2 / -3 sequence that does not end the round."""
+        self.ctx.call("nfsp_env_round_status", native.ptr(self._small))
+        v = int(self._small[0].item())
+        return True if v == 1 else (None if v == 255 else False)
+
     def step(self, action, p_index):
         p = int(p_index)
         a = np.asarray(action, dtype=np.float32).reshape(3)

@@ -75,6 +75,8 @@ SIGNATURES = {
     "nfsp_env_get_state": (I32, [P, I32, P, P, P, P, P, P]),
     "nfsp_env_step": (I32, [P, P, I32, P, P]),
     "nfsp_env_round": (I32, [P, P]),
+    "nfsp_env_do_action": (I32, [P, P, I32, P, P, P]),
+    "nfsp_env_round_status": (I32, [P, P]),
     "nfsp_env_export": (I32, [P, P]),
     "nfsp_mlp_forward": (I32, [P, P, I32, I32, P, P, I64]),
     "nfsp_mlp_fit": (I32, [P, P, I32, I32, P, P, I32, P, I32, I32, F32]),

@@ -23,6 +23,7 @@ Outputs (all ``numpy.savez_compressed``, no pickles):
   buffers_trace.npz  ReplayBuffer / ReservoirBuffer insert + sample traces
   rollout_trace.npz  main.train + agent.py event log (hands, get_state, step, inserts,
                      samples, updates, schedules)
+  do_action_kat.npz  Env.do_action / game_or_round_has_terminated called directly
 
 Usage: python tests/golden/gen_golden.py   (CWD anywhere; writes next to this file)
 """
@@ -429,6 +430,56 @@ def gen_rollout(dk, ne, rb, rs, ag, mn):
     print("rollout_trace:", len(code), "events", counts)
 
 
+# ---------------------------------------------------------------------------
+# 5. do_action / game_or_round_has_terminated called directly
+# ---------------------------------------------------------------------------
+DO_VECS = np.array([[1, 0, 0], [0, 1, 0], [0, 0, 1], [0, 0.5, 0.5], [1, 0, 1]], np.float64)
+
+
+def gen_do_action(dk, ne):
+    """leduc/newenv.py:131-190 called directly (not through step): every sequence of 1..3
+    do_action calls (vectors DO_VECS, players alternating from the dealer) from a fresh
+    hand (round 0) and from round 1 (reached by step([C]), step([C])), both dealers.  Per
+    call: do_action's return, game_or_round_has_terminated() (1 True, 0 False, -1 None),
+    and the env state it changed."""
+    import itertools
+    os.chdir(REF)
+    env = ne.Env()
+    rows = dict(hand=[], dealer=[], pre=[], p=[], vec=[], fold=[], status=[], hist=[], pot_half=[],
+                raises=[], round_raises=[], la=[])
+    h = 0
+    for dealer in (0, 1):
+        for pre in (0, 1):
+            for L in (1, 2, 3):
+                for seq in itertools.product(range(len(DO_VECS)), repeat=L):
+                    dk.rshuffle = rigged_shuffle((0, 1, 2))
+                    env.reset(dealer)
+                    p = dealer
+                    if pre:
+                        env.step(DO_VECS[1].reshape(1, 1, 3), p)
+                        env.step(DO_VECS[1].reshape(1, 1, 3), 1 - p)
+                        assert env.round_index == 1 and not env.terminated
+                    for v in seq:
+                        f = env.do_action(DO_VECS[v].reshape(1, 1, 3), p)
+                        st = env.game_or_round_has_terminated()
+                        flat = env.history.flatten()
+                        rows["hand"].append(h); rows["dealer"].append(dealer); rows["pre"].append(pre)
+                        rows["p"].append(p); rows["vec"].append(v); rows["fold"].append(bool(f))
+                        rows["status"].append(1 if st is True else (-1 if st is None else 0))
+                        rows["hist"].append(sum(1 << i for i in range(24) if flat[i]))
+                        rows["pot_half"].append([int(round(2 * x)) for x in env.overall_raises])
+                        rows["raises"].append([int(x) for x in env.raises])
+                        rows["round_raises"].append(int(env.round_raises))
+                        rows["la"].append(np.array(env.last_action[p], np.float64).reshape(3))   # a copy
+                        p = 1 - p
+                    h += 1
+    out = {k: np.asarray(v) for k, v in rows.items()}
+    out["vecs"] = DO_VECS
+    np.savez_compressed(os.path.join(HERE, "do_action_kat.npz"), **out)
+    print(f"do_action_kat: {h} sequences, {len(rows['hand'])} calls, "
+          f"status counts {np.unique(out['status'], return_counts=True)}")
+
+
 def main():
     import contextlib
     import io
@@ -442,4 +493,9 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["do_action"]:           # only the do_action fixture
+        os.chdir(REF)
+        _dk, _ne = load_reference_env()[1:]
+        gen_do_action(_dk, _ne)
+    else:
+        main()

@@ -94,3 +94,24 @@ def test_dropin_env_matches_oracle_with_global_random(pkg):
         s1 = env.get_state(1)[3].reshape(30)
         assert int(np.argmax(s0[24:27])) == ref[i][0]
         assert int(np.argmax(s1[24:27])) == ref[i][1]
+
+
+@pytest.mark.gpu
+def test_dropin_do_action_matches_reference_kat(pkg):
+    """Env.do_action / game_or_round_has_terminated called directly (do_action_kat.npz, made
+    by running the reference) through the drop-in Env: nfsp_env_do_action /
+    nfsp_env_round_status on the device; state read back from nfsp_env_export."""
+    from test_oracle_golden import _replay_do_action
+    leduc, native = pkg.leduc, pkg.native
+
+    def make(dealer):
+        e = leduc.Env(verbose=False)
+        e.reset(dealer, (0, 1, 2))
+        return e
+
+    def state(e, p):
+        e.ctx.call("nfsp_env_export", native.ptr(e._hand))
+        h = np.frombuffer(e._hand.cpu().numpy().tobytes(), dtype=leduc.HAND_DTYPE)[0]
+        return (int(h["hist"]) & 0xFFFFFF, (int(h["c0"]), int(h["c1"])),
+                (int(h["raises0"]), int(h["raises1"])), int(h["slot"]), h["la"][p])
+    assert _replay_do_action(make, state) == 1720
