@@ -19,8 +19,9 @@ def __getattr__(name):
 
 def install_dropin():
     """Register the reference's module names so main.py imports this engine unchanged:
-    ``leduc.newenv`` -> .leduc, ``agent.agent`` -> .agent, ``utils.replay_buffer`` /
-    ``utils.ReservoirBuffer`` -> .buffers."""
+    ``leduc.newenv`` -> .leduc, ``leduc.deck`` / ``leduc.cardmatrix`` -> .deck,
+    ``agent.agent`` -> .agent, ``utils.replay_buffer`` / ``utils.ReservoirBuffer`` -> .buffers
+    (see INTEGRATION.md)."""
     import importlib
     import sys
     import types
@@ -28,7 +29,11 @@ def install_dropin():
     le = importlib.import_module(".leduc", __name__)
     ag = importlib.import_module(".agent", __name__)
     bu = importlib.import_module(".buffers", __name__)
-    for top, sub, mod in (("leduc", "newenv", le), ("agent", "agent", ag),
+    dk = importlib.import_module(".deck", __name__)
+    cm = types.ModuleType("cardmatrix")
+    cm.Cardmatrix = dk.Cardmatrix
+    for top, sub, mod in (("leduc", "newenv", le), ("leduc", "deck", dk), ("leduc", "cardmatrix", cm),
+                          ("agent", "agent", ag),
                           ("utils", "replay_buffer", bu), ("utils", "ReservoirBuffer", bu)):
         parent = sys.modules.get(top) or types.ModuleType(top)
         parent.__path__ = []

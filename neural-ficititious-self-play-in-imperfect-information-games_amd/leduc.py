@@ -30,6 +30,7 @@ import random
 import numpy as np
 import torch
 
+from . import deck
 from . import native
 from . import pyrandom
 
@@ -51,10 +52,11 @@ def bits_to_obs(b: int) -> np.ndarray:
 
 
 def deal_from_global_random():
-    """One reference-deck shuffle with the global ``random`` (leduc/deck.py:35-44)."""
-    cards = list(range(6))          # deck order r0s0 r0s1 r1s0 r1s1 r2s0 r2s1
-    pyrandom.shuffle(cards)        # Python 3 (default) or 2.7 semantics: pyrandom
-    return cards[5] >> 1, cards[4] >> 1, cards[3] >> 1
+    """One reference deal (leduc/newenv.py:85-86,106-114,221): a new deck shuffled with the
+    global ``random``, then P0, P1 and the public card picked up from its end."""
+    d = deck.Deck(6)
+    d.shuffle()
+    return d.pick_up().rank, d.pick_up().rank, d.pick_up().rank
 
 
 class Env:

@@ -73,3 +73,22 @@ def test_dropin_deal_follows_the_mode(pr, pkg):
             pr.shuffle(cards)
             want.append((cards[5] >> 1, cards[4] >> 1, cards[3] >> 1))
         assert got == want
+
+
+def test_dropin_deck_deals_like_the_reference(pkg):
+    """leduc.deck (the drop-in Deck) against the reference's own deals (deal_seq.npz: the
+    reference Env reset + deck, CPython-3 random, 3 seeds): P0, P1 and the public card."""
+    from conftest import golden
+    pkg.pyrandom.set_python_semantics(3)
+    for seed in (1234, 7, 99):
+        ref = golden("deal_seq.npz")[f"seed{seed}"]
+        random.seed(seed)
+        for i in range(len(ref)):
+            d = pkg.deck.Deck()
+            d.shuffle()
+            got = (d.pick_up().rank, d.pick_up().rank, d.pick_up().rank)
+            assert got == tuple(int(x) for x in ref[i]), (seed, i)
+    c = pkg.deck.Card(0, 1)
+    assert c.rank == 0 and str(c) == "Ace Spades 0 1"
+    assert pkg.deck.Deck().fake_pub_card().rank == -1
+    assert len(pkg.deck.Deck()._cards) == 6
