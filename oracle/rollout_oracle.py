@@ -126,11 +126,13 @@ def deal_kuhn(j3, j2):
 
 
 def _one_lane(L, g, seed, w_flat, eps, eta, alias, game="leduc"):
-    key = id(w_flat)
-    if key not in _NETS_CACHE:
+    # the cache holds the weights object itself: an id() alone can be reused by a later
+    # array once the first is freed, which would replay lanes with stale nets
+    if _NETS_CACHE.get("w") is not w_flat:
         _NETS_CACHE.clear()
-        _NETS_CACHE[key] = Nets(w_flat)
-    nets = _NETS_CACHE[key]
+        _NETS_CACHE["w"] = w_flat
+        _NETS_CACHE["nets"] = Nets(w_flat)
+    nets = _NETS_CACHE["nets"]
     k0, k1 = U32(seed & 0xFFFFFFFF), U32((seed >> 32) & 0xFFFFFFFF)
     glo, ghi = U32(g & 0xFFFFFFFF), U32((g >> 32) & 0xFFFFFFFF)
     one = lambda v: np.array([v], U32)  # noqa: E731
