@@ -49,6 +49,7 @@ extern "C" {
 /* MLP output activation / loss (agent/agent.py:103,106,112,115) */
 #define NFSP_ACT_RELU 0        /* BR / target-BR head, Huber loss */
 #define NFSP_ACT_SOFTMAX 1     /* AR head, categorical cross-entropy */
+#define NFSP_ACT_LINEAR 2      /* BR head under NFSP_EXT_LINEAR_Q (engine only) */
 
 /* Reference quirks, reproduced by default (SURVEY.md §7 hard part (b)). */
 #define NFSP_QUIRK_TERMINAL_BOOTSTRAP 1u  /* `t_batch[k] is True` never holds: terminal
@@ -60,6 +61,21 @@ extern "C" {
                                              hand ends up with p's LAST pre-action s and a
                                              (utils/replay_buffer.py:30-41 + newenv.py:119) */
 #define NFSP_QUIRKS_REFERENCE 7u
+/* Textbook-NFSP extensions of the batched engine (Heinrich & Silver 2016), in the same
+ * cfg.quirks word.  NOT the reference's algorithm -- NFSP_QUIRKS_REFERENCE leaves them off.
+ * They let the same engine run NFSP proper, e.g. for C5's exploitability -> 0 check
+ * (DESIGN.md §9); quirks = NFSP_TEXTBOOK is that algorithm with every reference quirk off. */
+#define NFSP_EXT_SL_ONEHOT 8u     /* M_SL stores one-hot(argmax) of the BR action, not its raw
+                                     vector (the reference: agent/agent.py:147-151) */
+#define NFSP_EXT_RESERVOIR 16u    /* M_SL is a true reservoir (Algorithm R): the k-th insert
+                                     (k >= N, 0-based) takes slot j = U{0..k} iff j < N (the
+                                     reference: utils/ReservoirBuffer.py:22-28) */
+#define NFSP_EXT_LINEAR_Q 32u     /* BR / target nets with a linear Q head (the reference's is
+                                     ReLU, agent/agent.py:103); Huber on the linear outputs */
+#define NFSP_EXT_EPS_CONST 64u    /* eps stays at cfg.epsilon (the reference: eps / iteration
+                                     after each BR update, agent/agent.py:253, which ends
+                                     exploration within a few updates) */
+#define NFSP_TEXTBOOK (NFSP_EXT_SL_ONEHOT | NFSP_EXT_RESERVOIR | NFSP_EXT_LINEAR_Q | NFSP_EXT_EPS_CONST)
 
 typedef struct nfsp_ctx nfsp_ctx;
 

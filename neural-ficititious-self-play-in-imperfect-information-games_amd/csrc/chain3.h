@@ -167,6 +167,8 @@ __device__ inline floatx4 mfma3t(bf16x8 ahi, bf16x8 amid, bf16x8 alo, bf16x8 b) 
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, b, z, 0, 0, 0);
 }
 
+// RELU: 0 = the AR net (softmax, categorical cross-entropy), 1 = the BR net (ReLU Q head,
+// Huber), 2 = a BR net with a linear Q head (NFSP_EXT_LINEAR_Q, Huber).
 template <int RELU, int LOSS>
 __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -303,15 +305,15 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
       const float tt[3] = {tg.x, tg.y, tg.z};
       o_keep[0] = o0; o_keep[1] = o1; o_keep[2] = o2;
       tt_keep[0] = tg.x; tt_keep[1] = tg.y; tt_keep[2] = tg.z;
-      if (RELU) {          // Huber on ReLU outputs, mean over 3 x batch
+      if (RELU) {          // Huber on ReLU outputs (RELU 2: linear outputs), mean over 3 x batch
         const float oz[3] = {o0, o1, o2};
         float dd[3];
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-          const float ee = tt[k] - fmaxf(oz[k], 0.f);
+          const float ee = tt[k] - (RELU == 2 ? oz[k] : fmaxf(oz[k], 0.f));
           // |e| > 1 ? sign(e) : e  ==  clamp(e, -1, 1)
           const float gg = __builtin_amdgcn_fmed3f(ee, -1.f, 1.f);
-          dd[k] = oz[k] > 0.f ? gg * -inv3m : 0.f;
+          dd[k] = (RELU == 2 || oz[k] > 0.f) ? gg * -inv3m : 0.f;
         }
         d0 = dd[0]; d1 = dd[1]; d2 = dd[2];
       } else {
@@ -347,7 +349,7 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
       if (RELU) {          // huber_loss with py2's 1 / 2 == 0: |e| > 1 ? |e| : e^2 / 2, mean over 3
         float acc = 0.f;
         for (int k = 0; k < 3; ++k) {
-          const float e = tt_keep[k] - fmaxf(o_keep[k], 0.f);
+          const float e = tt_keep[k] - (RELU == 2 ? o_keep[k] : fmaxf(o_keep[k], 0.f));
           acc += fabsf(e) > 1.0f ? fabsf(e) : 0.5f * e * e;
         }
         Ls = acc * (1.0f / 3.0f);
@@ -503,6 +505,8 @@ inline int set_chain_lds(std::atomic<uint64_t>& mask, const void* f0, const void
 
 // AR chain launcher (chain_ar.hip): k_chain3<0, loss_log> on `s`, `blocks` workgroups.
 int launch_chain_ar(const ChainArgs& C, int blocks, bool loss_log, hipStream_t s);
+// BR chain with a linear Q head (NFSP_EXT_LINEAR_Q; chain_brlin.hip): k_chain3<2, loss_log>.
+int launch_chain_br_linear(const ChainArgs& C, bool loss_log, hipStream_t s);
 
 }  // namespace chain
 }  // namespace nfsp

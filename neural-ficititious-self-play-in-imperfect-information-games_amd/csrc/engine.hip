@@ -145,7 +145,7 @@ __global__ void __launch_bounds__(256) k_rollout(RolloutArgs A) {
           const u32x4 u = nfsp::philox4x32({(uint32_t)L, A.g_lo, A.g_hi, 2u + (uint32_t)dec}, A.k0, A.k1);
           dec++;
           if ((double)nfsp::u01(u.x) > (p ? eps1 : eps0)) {
-            fwd_lds(sw + (p * 2 + 1) * NET_LDS, x, NFSP_ACT_RELU, y);
+            fwd_lds(sw + (p * 2 + 1) * NET_LDS, x, br_act(A.quirks), y);
           } else {                 // np.random.rand(1, 1, 3)
             y[0] = nfsp::u01(u.y); y[1] = nfsp::u01(u.z); y[2] = nfsp::u01(u.w);
           }
@@ -156,9 +156,16 @@ __global__ void __launch_bounds__(256) k_rollout(RolloutArgs A) {
           const int k = nsl++;
           nslp[p]++;
           A.S.sl_x[k * N + L] = x;
-          A.S.sl_a[(k * 3 + 0) * N + L] = y[0];
-          A.S.sl_a[(k * 3 + 1) * N + L] = y[1];
-          A.S.sl_a[(k * 3 + 2) * N + L] = y[2];
+          if (A.quirks & NFSP_EXT_SL_ONEHOT) {   // the action taken (textbook NFSP)
+            const int v = nfsp::argmax3(y[0], y[1], y[2]);
+            A.S.sl_a[(k * 3 + 0) * N + L] = v == 0 ? 1.f : 0.f;
+            A.S.sl_a[(k * 3 + 1) * N + L] = v == 1 ? 1.f : 0.f;
+            A.S.sl_a[(k * 3 + 2) * N + L] = v == 2 ? 1.f : 0.f;
+          } else {
+            A.S.sl_a[(k * 3 + 0) * N + L] = y[0];
+            A.S.sl_a[(k * 3 + 1) * N + L] = y[1];
+            A.S.sl_a[(k * 3 + 2) * N + L] = y[2];
+          }
           A.S.sl_meta[k * N + L] = (uint32_t)p | ((uint32_t)nrlp[p] << 8);
         }
         act_pack += 1ull << (8 * (p * 3 + nfsp::argmax3(y[0], y[1], y[2])));

@@ -142,7 +142,11 @@ __device__ inline void stage_net_lds(float* sw, const float* __restrict__ w, int
 }
 
 // Forward of one 0/1 observation (bits) through a net staged by stage_net_lds.  Same
-// operation order as oracle/nn_oracle.py (bit-exact for the ReLU head).
+// operation order as oracle/nn_oracle.py (bit-exact for the ReLU and linear heads).
+// The BR / target head: ReLU (the reference) or linear (NFSP_EXT_LINEAR_Q).
+__host__ __device__ inline int br_act(unsigned quirks) {
+  return (quirks & NFSP_EXT_LINEAR_Q) ? NFSP_ACT_LINEAR : NFSP_ACT_RELU;
+}
 __device__ inline void fwd_lds(const float* __restrict__ sw, uint32_t x, int act, float y[3]) {
 #pragma clang fp contract(off)
   // the set bits' W1 rows in ascending order; the unused slots point at the zero row, so
@@ -184,6 +188,8 @@ __device__ inline void fwd_lds(const float* __restrict__ sw, uint32_t x, int act
     y[0] = o0 > 0.f ? o0 : 0.f;
     y[1] = o1 > 0.f ? o1 : 0.f;
     y[2] = o2 > 0.f ? o2 : 0.f;
+  } else if (act == NFSP_ACT_LINEAR) {
+    y[0] = o0; y[1] = o1; y[2] = o2;
   } else {
     const float m = fmaxf(fmaxf(o0, o1), o2);
     const float e0 = expf(o0 - m), e1 = expf(o1 - m), e2 = expf(o2 - m);

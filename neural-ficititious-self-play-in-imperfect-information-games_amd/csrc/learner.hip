@@ -50,6 +50,7 @@ struct PrepArgs {
   int B, E;
   uint32_t k0, k1, tag;
   float lr_ar;
+  uint32_t quirks;
 };
 
 // ---------------------------------------------------------------------------
@@ -107,7 +108,9 @@ __global__ void __launch_bounds__(256) k_ar_slots(PrepArgs P) {
     const u32x4 r = nfsp::philox4x32({TAG_RES | (uint32_t)a, (uint32_t)tot, (uint32_t)(tot >> 32), 0u},
                                      P.k0, P.k1);
     const uint64_t r64 = ((uint64_t)r.x << 32) | r.y;
-    const int64_t j = 1 + (int64_t)(r64 % (uint64_t)cap);        // randrange(1, N + 1)
+    const int64_t j = (P.quirks & NFSP_EXT_RESERVOIR)
+                          ? (int64_t)(r64 % (uint64_t)(tot + 1))  // Algorithm R: U{0..tot}
+                          : 1 + (int64_t)(r64 % (uint64_t)cap);   // randrange(1, N + 1)
     slot = j < cap ? j : -1;                                     // replace iff j < N
   }
   const int64_t qi = (int64_t)a * P.M.pend_cap + q;
@@ -302,12 +305,12 @@ __global__ void __launch_bounds__(256) k_br_targets(LearnBufs LB, const float* _
   if (b < B) {
     float y[3];
     if (!s2half) {
-      fwd_lds(sw, rr.s, NFSP_ACT_RELU, y);
+      fwd_lds(sw, rr.s, br_act(quirks), y);
       q[b][0] = y[0]; q[b][1] = y[1]; q[b][2] = y[2];
       am[b] = (uint8_t)(rr.meta & 0xFFu);
       sb[b] = rr.s;
     } else {
-      fwd_lds(sw, rr.s2, NFSP_ACT_RELU, y);
+      fwd_lds(sw, rr.s2, br_act(quirks), y);
       const float qmax = fmaxf(fmaxf(y[0], y[1]), y[2]);
       const float r = (float)(int8_t)((rr.meta >> 16) & 0xFFu) * 0.5f;
       const bool terminal = !(quirks & NFSP_QUIRK_TERMINAL_BOOTSTRAP) && ((rr.meta >> 8) & 1u);
@@ -422,6 +425,7 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
   P.k1 = (uint32_t)(cfg.seed >> 32);
   P.tag = e->learn_tag;
   P.lr_ar = cfg.lr_ar;
+  P.quirks = cfg.quirks;
   int64_t maxU = 0, maxUbr = 0, maxSL = 0;
   for (int a = 0; a < 2; ++a) {
     AgentPlan& pl = P.A[a];
@@ -559,8 +563,13 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
       C.u1[0] = v;
       {
         KTimer kc(e, KT_CHAIN_BR, sa);
-        if (C.loss_out) k_chain3<1, 1><<<1, 256, CHAIN_LDS, sa>>>(C);
-        else k_chain3<1, 0><<<1, 256, CHAIN_LDS, sa>>>(C);
+        if (cfg.quirks & NFSP_EXT_LINEAR_Q) {
+          const int rc = launch_chain_br_linear(C, C.loss_out != nullptr, sa);
+          if (rc != NFSP_OK) return rc;
+        } else {
+          if (C.loss_out) k_chain3<1, 1><<<1, 256, CHAIN_LDS, sa>>>(C);
+          else k_chain3<1, 0><<<1, 256, CHAIN_LDS, sa>>>(C);
+        }
       }
       NFSP_LAUNCHED("k_chain(BR)");
       u = v;
@@ -570,7 +579,7 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
       if (tc % cfg.target_every == 0) syncs++;
       tc++;
       it += 2;
-      eps = eps / (double)it;
+      eps = (cfg.quirks & NFSP_EXT_EPS_CONST) ? cfg.epsilon : eps / (double)it;
     }
     F.iteration[a] = it;
     F.tcount[a] = tc;

@@ -84,8 +84,12 @@ def draw_perm(batch, e, stream, m, k0, k1):
     return out
 
 
-def reservoir_slots(a, sl_total0, n_sl, cap, k0, k1):
-    """Slot of each SL insert of the rollout (-1: not stored)."""
+EXT_RESERVOIR, EXT_LINEAR_Q, EXT_EPS_CONST = 16, 32, 64      # include/nfsp.h NFSP_EXT_*
+
+
+def reservoir_slots(a, sl_total0, n_sl, cap, k0, k1, ext=0):
+    """Slot of each SL insert of the rollout (-1: not stored).  ext & EXT_RESERVOIR: a true
+    reservoir (Algorithm R, j = U{0..tot}) instead of the reference's randrange(1, N + 1)."""
     slots = np.empty(n_sl, np.int64)
     for q in range(n_sl):
         tot = sl_total0 + q
@@ -94,7 +98,8 @@ def reservoir_slots(a, sl_total0, n_sl, cap, k0, k1):
         else:
             x, y, _, _ = philox4x32(np.uint32(TAG_RES | a), np.uint32(tot & M32), np.uint32((tot >> 32) & M32),
                                     np.uint32(0), k0, k1)
-            j = 1 + ((int(x) << 32) | int(y)) % cap
+            r64 = (int(x) << 32) | int(y)
+            j = r64 % (tot + 1) if ext & EXT_RESERVOIR else 1 + r64 % cap
             slots[q] = j if j < cap else -1
     return slots
 
@@ -131,8 +136,9 @@ def learner_step(cfg, state, quirks=7):
         U_br = max(0, m_last - m_br0 + 1)
         log_cap = len(st["rl_s_bits"])
         ar = nn.MLP(nn.ACT_SOFTMAX, 64, weights=nn.unpack_weights(st["w"][0]))
-        br = nn.MLP(nn.ACT_RELU, 64, weights=nn.unpack_weights(st["w"][1]))
-        tg = nn.MLP(nn.ACT_RELU, 64, weights=nn.unpack_weights(st["w"][2]))
+        br_act = nn.ACT_LINEAR if quirks & EXT_LINEAR_Q else nn.ACT_RELU
+        br = nn.MLP(br_act, 64, weights=nn.unpack_weights(st["w"][1]))
+        tg = nn.MLP(br_act, 64, weights=nn.unpack_weights(st["w"][2]))
         it, tc, eps = st["iteration"], st["br_updates"], st["epsilon"]
         it0 = it
         expl = None
@@ -159,12 +165,12 @@ def learner_step(cfg, state, quirks=7):
             if (tc + u) % cfg["target_every"] == 0:
                 tg.set_weights(br.get_weights())
             it += 2
-            eps = eps / it
+            eps = cfg["epsilon"] if quirks & EXT_EPS_CONST else eps / it
         # ---- AR updates, the reservoir as of each trigger
         n_sl = st["last_sl"]
         sl0 = st["sl_total"] - n_sl
         cap = cfg["sl_capacity"]
-        slots = reservoir_slots(a, sl0, n_sl, cap, k0, k1)
+        slots = reservoir_slots(a, sl0, n_sl, cap, k0, k1, quirks)
         pos = np.asarray(st["pend_pos"][:n_sl], np.int64)
         n_ar = 0
         for u in range(U):

@@ -35,6 +35,7 @@ N_IN, N_OUT = 30, 3
 
 ACT_RELU = 0              # BR / target-BR output activation (agent/agent.py:103)
 ACT_SOFTMAX = 1           # AR output activation (agent/agent.py:112)
+ACT_LINEAR = 2            # BR head under the engine's NFSP_EXT_LINEAR_Q (not the reference)
 
 
 def glorot_uniform(rng: np.random.RandomState, fan_in: int, fan_out: int) -> np.ndarray:
@@ -97,6 +98,8 @@ class MLP:
         z2 = dense_seq(h, self.W2, self.b2)
         if self.act == ACT_RELU:
             y = np.maximum(z2, F32(0))
+        elif self.act == ACT_LINEAR:
+            y = z2
         else:
             y = softmax3(z2)
         return z1, h, z2, y.astype(F32)
@@ -113,12 +116,12 @@ class MLP:
         """Gradients of the Keras loss of this head on one minibatch."""
         m = x2d.shape[0]
         z1, h, z2, y = self._forward(x2d)
-        if self.act == ACT_RELU:
+        if self.act in (ACT_RELU, ACT_LINEAR):
             # Huber (agent/agent.py:91-99); mean over the 3 outputs, then over the batch.
             e = t2d - y
             dldy = np.where(np.abs(e) > F32(1.0), np.sign(e), e).astype(F32)
             dldy = -dldy / F32(3 * m)
-            dz2 = dldy * (z2 > 0).astype(F32)
+            dz2 = dldy * (z2 > 0).astype(F32) if self.act == ACT_RELU else dldy
         else:
             # categorical_crossentropy, TF backend, from_logits=False.
             S = y.sum(axis=-1, keepdims=True)
@@ -145,7 +148,7 @@ class MLP:
         softmax, mean over the batch."""
         y = self._forward(x2d)[3].astype(np.float64)
         t = t2d.astype(np.float64)
-        if self.act == ACT_RELU:
+        if self.act in (ACT_RELU, ACT_LINEAR):
             e = t - y
             v = np.where(np.abs(e) > 1.0, np.abs(e), 0.5 * e * e)
             return float(v.mean(axis=-1).mean())

@@ -73,13 +73,16 @@ def deal_from_draws(j5, j4, j3):
     return d[5] >> 1, d[4] >> 1, d[3] >> 1
 
 
+EXT_SL_ONEHOT, EXT_RESERVOIR, EXT_LINEAR_Q, EXT_EPS_CONST = 8, 16, 32, 64   # include/nfsp.h
+
+
 class Nets:
     """The four acting heads of a rollout from the engine's packed [2][3][NP] weights."""
 
-    def __init__(self, w_flat):
+    def __init__(self, w_flat, br_act=nn.ACT_RELU):
         w = np.asarray(w_flat, np.float32).reshape(2, 3, -1)
         self.ar = [nn.MLP(nn.ACT_SOFTMAX, 64, weights=nn.unpack_weights(w[a, 0])) for a in (0, 1)]
-        self.br = [nn.MLP(nn.ACT_RELU, 64, weights=nn.unpack_weights(w[a, 1])) for a in (0, 1)]
+        self.br = [nn.MLP(br_act, 64, weights=nn.unpack_weights(w[a, 1])) for a in (0, 1)]
 
 
 def orc_bits(x) -> int:
@@ -88,10 +91,10 @@ def orc_bits(x) -> int:
 
 
 def rollout_with_positions(n_lanes, g, seed, w_flat, eps, eta=0.1, alias=True, rl_before=(0, 0),
-                           game="leduc"):
+                           game="leduc", ext=0):
     """rollout() plus, for each SL record, its global RL stream position (what the engine
-    stores in its pending list)."""
-    out = rollout_lanes(n_lanes, g, seed, w_flat, eps, eta, alias, game)
+    stores in its pending list).  ``ext``: the engine's NFSP_EXT_* bits (include/nfsp.h)."""
+    out = rollout_lanes(n_lanes, g, seed, w_flat, eps, eta, alias, game, ext)
     rl = ([], [])
     sl = ([], [])
     base = list(rl_before)
@@ -104,13 +107,13 @@ def rollout_with_positions(n_lanes, g, seed, w_flat, eps, eta=0.1, alias=True, r
     return dict(rl=rl, sl=sl, actions=out["actions"], reward=out["reward"])
 
 
-def rollout_lanes(n_lanes, g, seed, w_flat, eps, eta=0.1, alias=True, game="leduc"):
+def rollout_lanes(n_lanes, g, seed, w_flat, eps, eta=0.1, alias=True, game="leduc", ext=0):
     """Like rollout() but keeps the records per lane."""
     lanes = []
     actions = np.zeros((2, 3), np.int64)
     reward = np.zeros(2)
     for L in range(n_lanes):
-        res = _one_lane(L, g, seed, w_flat, eps, eta, alias, game)
+        res = _one_lane(L, g, seed, w_flat, eps, eta, alias, game, ext)
         lanes.append(res)
         actions += res["actions"]
         reward += res["reward"]
@@ -125,13 +128,15 @@ def deal_kuhn(j3, j2):
     return int(j3), int((j3 + 1 + j2) % 3), 0
 
 
-def _one_lane(L, g, seed, w_flat, eps, eta, alias, game="leduc"):
+def _one_lane(L, g, seed, w_flat, eps, eta, alias, game="leduc", ext=0):
     # the cache holds the weights object itself: an id() alone can be reused by a later
     # array once the first is freed, which would replay lanes with stale nets
-    if _NETS_CACHE.get("w") is not w_flat:
+    br_act = nn.ACT_LINEAR if ext & EXT_LINEAR_Q else nn.ACT_RELU
+    if _NETS_CACHE.get("w") is not w_flat or _NETS_CACHE.get("br_act") != br_act:
         _NETS_CACHE.clear()
         _NETS_CACHE["w"] = w_flat
-        _NETS_CACHE["nets"] = Nets(w_flat)
+        _NETS_CACHE["br_act"] = br_act
+        _NETS_CACHE["nets"] = Nets(w_flat, br_act)
     nets = _NETS_CACHE["nets"]
     k0, k1 = U32(seed & 0xFFFFFFFF), U32((seed >> 32) & 0xFFFFFFFF)
     glo, ghi = U32(g & 0xFFFFFFFF), U32((g >> 32) & 0xFFFFFFFF)
@@ -177,7 +182,10 @@ def _one_lane(L, g, seed, w_flat, eps, eta, alias, game="leduc"):
                 y = np.array([u01(c[1]), u01(c[2]), u01(c[3])], np.float32)
         env.step(np.asarray(y, np.float64).reshape(1, 1, 3), p)
         if pol_br[p]:
-            sl[p].append((orc_bits(x), np.asarray(y, np.float32).copy(), n_rl_p[p]))
+            ysl = np.asarray(y, np.float32).copy()
+            if ext & EXT_SL_ONEHOT:          # the action taken (textbook NFSP)
+                ysl = np.eye(3, dtype=np.float32)[int(np.argmax(ysl))]
+            sl[p].append((orc_bits(x), ysl, n_rl_p[p]))
         actions[p][int(np.argmax(y))] += 1
         return False
 

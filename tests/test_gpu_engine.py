@@ -60,14 +60,14 @@ def check_rollout(eng, ref, rl_before=(0, 0)):
         assert np.array_equal(pp, np.array([e[2] for e in ref["sl"][p]]))
 
 
-@pytest.mark.parametrize("quirks", [7, 3])
+@pytest.mark.parametrize("quirks", [7, 3, 120])      # 120: NFSP_TEXTBOOK (one-hot SL, linear Q)
 def test_rollout_matches_oracle(pkg, quirks):
     N, seed = 3000, 1234
     eng = engine(pkg, n_lanes=N, seed=seed, quirks=quirks, init_seed=11, eta=0.3,
                  inserts_per_update=1 << 30)
     w = weights_flat(eng)
     eng.rollout()
-    ref = R.rollout_with_positions(N, 0, seed, w, (0.06, 0.06), eta=0.3, alias=bool(quirks & 4))
+    ref = R.rollout_with_positions(N, 0, seed, w, (0.06, 0.06), eta=0.3, alias=bool(quirks & 4), ext=quirks)
     check_rollout(eng, ref)
     st = eng.stats()
     assert np.array_equal(np.array(st["actions"]), ref["actions"])
@@ -78,7 +78,7 @@ def test_rollout_matches_oracle(pkg, quirks):
     before = tuple(eng.stats()["rl_total"])
     eng.rollout()
     ref2 = R.rollout_with_positions(N, 1, seed, w, (0.06, 0.06), eta=0.3, alias=bool(quirks & 4),
-                                    rl_before=before)
+                                    rl_before=before, ext=quirks)
     check_rollout(eng, ref2, rl_before=before)
 
 
