@@ -33,3 +33,30 @@ def test_reservoir_slots_append_then_replace():
     sl = LO.reservoir_slots(1, 40, 30, cap, 3, 4)
     assert sl[:10].tolist() == list(range(40, 50))          # append while count < N
     assert all(-1 <= v < cap and v != 0 for v in sl[10:])    # j in [1, N], kept iff j < N
+
+
+def test_reservoir_slots_algorithm_r_is_uniform():
+    """NFSP_EXT_RESERVOIR (Algorithm R): after K inserts into N slots every insert survives
+    with probability N / K; the reference's rule (utils/ReservoirBuffer.py:22-28) replaces on
+    almost every insert, so its survivors are the last few hundred."""
+    cap, K, trials = 40, 400, 120
+    early_tb = late_tb = early_ref = 0
+    for t in range(trials):
+        for ext, acc in ((LO.EXT_RESERVOIR, "tb"), (0, "ref")):
+            slots = LO.reservoir_slots(0, 0, K, cap, 1000 + t, 7, ext)
+            owner = np.arange(cap)
+            for q in range(cap, K):
+                if slots[q] >= 0:
+                    owner[slots[q]] = q
+            kept = set(owner.tolist())
+            early = sum(q in kept for q in range(1, 101))   # item 0 sits in the reference's
+            # never-replaced slot 0
+            late = sum(q in kept for q in range(K - 100, K))
+            if acc == "tb":
+                early_tb += early
+                late_tb += late
+            else:
+                early_ref += early
+    p = cap / K                          # 0.1 per insert
+    assert abs(early_tb / (100 * trials) - p) < 0.02 and abs(late_tb / (100 * trials) - p) < 0.02
+    assert early_ref / (100 * trials) < 0.005
