@@ -75,7 +75,13 @@ extern "C" {
 #define NFSP_EXT_EPS_CONST 64u    /* eps stays at cfg.epsilon (the reference: eps / iteration
                                      after each BR update, agent/agent.py:253, which ends
                                      exploration within a few updates) */
-#define NFSP_TEXTBOOK (NFSP_EXT_SL_ONEHOT | NFSP_EXT_RESERVOIR | NFSP_EXT_LINEAR_Q | NFSP_EXT_EPS_CONST)
+#define NFSP_EXT_SAMPLE_AR 128u   /* an agent acting with its average policy samples the action
+                                     from the AR softmax (Philox counter (lane, hand, 2^31 + k)
+                                     for its k-th AR decision) and passes the one-hot vector:
+                                     the reference passes the softmax itself, which the env
+                                     executes as its argmax (agent/agent.py:143, newenv.py:135) */
+#define NFSP_TEXTBOOK (NFSP_EXT_SL_ONEHOT | NFSP_EXT_RESERVOIR | NFSP_EXT_LINEAR_Q | \
+                       NFSP_EXT_EPS_CONST | NFSP_EXT_SAMPLE_AR)
 
 typedef struct nfsp_ctx nfsp_ctx;
 

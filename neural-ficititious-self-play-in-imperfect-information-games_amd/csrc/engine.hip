@@ -90,7 +90,7 @@ __global__ void __launch_bounds__(256) k_rollout(RolloutArgs A) {
     nfsp::hand_reset(h, dealer, r0, r1, rp, A.game);
     const bool alias = (A.quirks & NFSP_QUIRK_ALIAS_RL) != 0;
     int nrl = 0, nsl = 0, nrlp[2] = {0, 0}, nslp[2] = {0, 0};
-    int dec = 0;
+    int dec = 0, dec_ar = 0;
     uint64_t act_pack = 0;       // 6 x 8-bit action counters (agent*3 + action)
     int rew_half[2] = {0, 0};
     // main.train scheduler (main.py:55-67) as phases of one while-iteration
@@ -141,6 +141,14 @@ __global__ void __launch_bounds__(256) k_rollout(RolloutArgs A) {
         float y[3];
         if (!polBR[p]) {
           fwd_lds(sw + (p * 2 + 0) * NET_LDS, x, NFSP_ACT_SOFTMAX, y);
+          if (A.quirks & NFSP_EXT_SAMPLE_AR) {   // sample the average policy (textbook NFSP)
+            const u32x4 u = nfsp::philox4x32({(uint32_t)L, A.g_lo, A.g_hi, 0x80000000u + (uint32_t)dec_ar},
+                                             A.k0, A.k1);
+            dec_ar++;
+            const float r = nfsp::u01(u.x);
+            const int v = r < y[0] ? 0 : (r < y[0] + y[1] ? 1 : 2);
+            y[0] = v == 0 ? 1.f : 0.f; y[1] = v == 1 ? 1.f : 0.f; y[2] = v == 2 ? 1.f : 0.f;
+          }
         } else {
           const u32x4 u = nfsp::philox4x32({(uint32_t)L, A.g_lo, A.g_hi, 2u + (uint32_t)dec}, A.k0, A.k1);
           dec++;

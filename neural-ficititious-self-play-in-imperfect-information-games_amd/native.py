@@ -19,8 +19,8 @@ ACT_RELU, ACT_SOFTMAX = 0, 1
 QUIRK_TERMINAL_BOOTSTRAP, QUIRK_ROW0_TARGET, QUIRK_ALIAS_RL = 1, 2, 4
 QUIRKS_REFERENCE = 7
 # textbook-NFSP extensions (include/nfsp.h NFSP_EXT_*; not the reference's algorithm)
-EXT_SL_ONEHOT, EXT_RESERVOIR, EXT_LINEAR_Q, EXT_EPS_CONST = 8, 16, 32, 64
-TEXTBOOK = EXT_SL_ONEHOT | EXT_RESERVOIR | EXT_LINEAR_Q | EXT_EPS_CONST
+EXT_SL_ONEHOT, EXT_RESERVOIR, EXT_LINEAR_Q, EXT_EPS_CONST, EXT_SAMPLE_AR = 8, 16, 32, 64, 128
+TEXTBOOK = EXT_SL_ONEHOT | EXT_RESERVOIR | EXT_LINEAR_Q | EXT_EPS_CONST | EXT_SAMPLE_AR
 
 P = C.c_void_p
 I32, I64, U32, U64, F32, F64 = C.c_int, C.c_int64, C.c_uint, C.c_uint64, C.c_float, C.c_double

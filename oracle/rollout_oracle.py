@@ -73,7 +73,7 @@ def deal_from_draws(j5, j4, j3):
     return d[5] >> 1, d[4] >> 1, d[3] >> 1
 
 
-EXT_SL_ONEHOT, EXT_RESERVOIR, EXT_LINEAR_Q, EXT_EPS_CONST = 8, 16, 32, 64   # include/nfsp.h
+EXT_SL_ONEHOT, EXT_RESERVOIR, EXT_LINEAR_Q, EXT_EPS_CONST, EXT_SAMPLE_AR = 8, 16, 32, 64, 128   # nfsp.h
 
 
 class Nets:
@@ -160,6 +160,7 @@ def _one_lane(L, g, seed, w_flat, eps, eta, alias, game="leduc", ext=0):
     actions = np.zeros((2, 3), np.int64)
     reward = np.zeros(2)
     dec = [0]
+    dec_ar = [0]
 
     def play(p, initial):
         if not initial:
@@ -173,6 +174,12 @@ def _one_lane(L, g, seed, w_flat, eps, eta, alias, game="leduc", ext=0):
         x = env.obs(p).reshape(1, 1, 30)
         if not pol_br[p]:
             y = nets.ar[p].predict(x).reshape(3)
+            if ext & EXT_SAMPLE_AR:          # sample the average policy (textbook NFSP)
+                c = [v[0] for v in philox4x32(one(L), one(glo), one(ghi), one(0x80000000 + dec_ar[0]), k0, k1)]
+                dec_ar[0] += 1
+                r = np.float32(u01(c[0]))
+                v = 0 if r < y[0] else (1 if r < np.float32(y[0] + y[1]) else 2)
+                y = np.eye(3, dtype=np.float32)[v]
         else:
             c = [v[0] for v in philox4x32(one(L), one(glo), one(ghi), one(2 + dec[0]), k0, k1)]
             dec[0] += 1

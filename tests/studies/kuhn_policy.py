@@ -48,3 +48,41 @@ for a in (0, 1):
                 q = br.predict(x.reshape(1, 1, 30)).reshape(3)
                 print(f"agent {a} {'first ' if first else 'second'} hist {''.join(names[s] for s in seq):3s} card {'AKQ'[card]}: "
                       f"AR F {p[0]:.3f} C {p[1]:.3f} B {p[2]:.3f} | Q {q[0]:+.2f} {q[1]:+.2f} {q[2]:+.2f}")
+
+
+def memory_probe(eng, agent, dealer, card, seq, p_act=(1, 2)):
+    """Mean reward and count of the M_RL transitions of `agent` from the information state
+    (dealer, card, history seq) with a call / raise recorded (the last 200k inserts)."""
+    import torch
+    st = eng.stats()
+    m = eng.memories(agent)
+    n = int(min(st["rl_total"][agent], eng.cfg.rl_capacity))
+    rows = (torch.arange(int(st["rl_total"][agent]) - n, int(st["rl_total"][agent]), device=m["rl_s"].device)
+            % m["log_cap"])
+    w = torch.ones(30, dtype=torch.int64, device=rows.device) << torch.arange(30, device=rows.device)
+    sb = ((m["rl_s"][rows] != 0).long() * w).sum(1).cpu().numpy()
+    act = m["rl_a"][rows].argmax(1).cpu().numpy()
+    r = m["rl_r"][rows].cpu().numpy()
+    other = (card + 1) % 3
+    ranks = (card, other, 0) if agent == 0 else (other, card, 0)
+    x = obs(dealer, ranks, seq, agent).reshape(30)
+    want = int(sum(1 << i for i in range(30) if x[i]))
+    sel = (sb == want) & np.isin(act, p_act)
+    return int(sel.sum()), float(r[sel].mean()) if sel.any() else None
+
+
+if len(sys.argv) > 1:
+    for a, d in ((0, 0), (1, 1)):
+        for card in (1,):
+            print("memory", a, "dealer", d, "card K hist CB call:", memory_probe(eng, a, d, card, [1, 2]))
+
+if len(sys.argv) > 1:
+    for card in (0, 1, 2):
+        counts = [memory_probe(eng, 0, 1, card, [1], p_act=(k,))[0] for k in (0, 1, 2)]
+        print("memory agent 0 second (dealer 1) after check, card", "AKQ"[card], "F/C/B counts", counts)
+
+if len(sys.argv) > 1:
+    for card in (0, 2):
+        for k in (1, 2):
+            print("memory agent 0 second (dealer 1) after check, card", "AKQ"[card], "action", "FCB"[k],
+                  "(count, mean r):", memory_probe(eng, 0, 1, card, [1], p_act=(k,)))

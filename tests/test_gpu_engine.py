@@ -60,7 +60,8 @@ def check_rollout(eng, ref, rl_before=(0, 0)):
         assert np.array_equal(pp, np.array([e[2] for e in ref["sl"][p]]))
 
 
-@pytest.mark.parametrize("quirks", [7, 3, 120])      # 120: NFSP_TEXTBOOK (one-hot SL, linear Q)
+@pytest.mark.parametrize("quirks", [7, 3, 120, 248])  # 120: one-hot SL, reservoir, linear Q, const eps;
+                                                       # 248 = NFSP_TEXTBOOK (+ sampled AR actions)
 def test_rollout_matches_oracle(pkg, quirks):
     N, seed = 3000, 1234
     eng = engine(pkg, n_lanes=N, seed=seed, quirks=quirks, init_seed=11, eta=0.3,

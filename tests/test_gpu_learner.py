@@ -62,10 +62,11 @@ def _snapshot(eng):
 @pytest.mark.gpu
 @pytest.mark.parametrize("case,quirks", [("leduc", 7), ("leduc", 0), ("tiny_memories", 7), ("kuhn", 7),
                                          ("batch64_e3", 7),
-                                         # textbook-NFSP extensions (NFSP_TEXTBOOK = 120; 112 =
-                                         # without the one-hot SL targets)
+                                         # textbook-NFSP extensions (NFSP_TEXTBOOK = 248; 120 =
+                                         # without sampled AR actions, 112 = also without the
+                                         # one-hot SL targets)
                                          ("leduc", 120), ("leduc", 112), ("tiny_memories", 120),
-                                         ("kuhn", 120)])
+                                         ("kuhn", 120), ("kuhn", 248)])
 def test_learner_step_matches_oracle(pkg, case, quirks):
     cfg_e, game = CASES[case]
     g = pkg.native.GAME_KUHN if game == "kuhn" else pkg.native.GAME_LEDUC
