@@ -446,6 +446,8 @@ extern "C" int nfsp_engine_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, nfs
                "capacities must exceed the batch");
   NFSP_REQUIRE(cfg->sl_capacity < (1ll << 40) && cfg->rl_capacity < (1ll << 40), "capacity too large");
   NFSP_REQUIRE(cfg->inserts_per_update >= 1 && cfg->target_every >= 1, "bad cadence");
+  NFSP_REQUIRE((cfg->quirks & ~(NFSP_QUIRKS_REFERENCE | NFSP_TEXTBOOK)) == 0,
+               "unknown bits in quirks (NFSP_QUIRK_* | NFSP_EXT_*)");
   *out = nullptr;
   nfsp_engine* e = new nfsp_engine();
   e->ctx = ctx;

@@ -217,3 +217,11 @@ def test_device_views_keep_the_engine_alive(pkg):
     del w, m
     gc.collect()
     assert ref() is None
+
+
+def test_engine_rejects_unknown_quirk_bits(pkg):
+    with pytest.raises(pkg.native.NativeError, match="unknown bits"):
+        pkg.engine.SelfPlayEngine(n_lanes=64, quirks=256)
+    eng = pkg.engine.SelfPlayEngine(n_lanes=64, quirks=pkg.native.QUIRKS_REFERENCE | pkg.native.TEXTBOOK)
+    eng.step()
+    assert eng.stats()["hands"] == 64
