@@ -18,11 +18,19 @@ scaling), and once per engine step an RCCL all-reduce of the average-policy (AR)
 steps of both agents (shards.AvgPolicyAllReduce, 17.4 KB; `--ar-allreduce off` = independent
 replicas).  A barrier and a max-over-ranks of the elapsed time bracket the timed region.
 
-Roofline: HIP events recorded on the engine's stream around every kernel launch give
-each kernel's average duration; the dominant kernel's algorithmic FLOPs (or bytes) per
-launch / that duration is `roofline.achieved`.  The chains are latency-bound SGD steps: they
-are priced in MFMA FLOPs, and `roofline_other.k_chain3_br_hbm` gives the same kernel in
-SURVEY 8(d)'s HBM framing (128 sampled M_RL tuples x 257 B per update).
+Timing: W warmup steps, then K steps with no instrumentation -> `value` / `ms_per_step`;
+then K more steps with HIP events recorded on each kernel's stream around every launch ->
+each kernel's average duration (`kernel_ms`, `ms_per_step_event_timed`).
+
+Roofline: SURVEY 8(d)'s HBM framing of the dominant kernel (largest GPU time): algorithmic
+bytes per launch (the 128 sampled tuples of each update in the reference's fp32 layout,
+257 B M_RL / 132 B M_SL; the rollout: its inserted tuples) / its average duration.  The
+chains are latency-bound SGD steps, so `roofline_other` also prices them in MFMA FLOPs and
+as an issue roofline (static issue cycles per step / measured), and `whole_step_hbm_per_gpu`
+is SURVEY 8(d)'s whole-path bytes per hand x hands / step time.
+
+`bench.py --gpus N` without a torch.distributed environment starts the N rank processes
+itself (launch_ranks; the parent never touches a GPU); every rank checks WORLD_SIZE == N.
 
 `cpu_baseline` (rank 0, N = 1 only) comes from the C++ restatement of the reference's
 main.train (oracle/nfsp_cpu.cpp).  It uses the reference cadence and this config's memory
@@ -177,6 +185,60 @@ def job_value(units_per_rank, world, elapsed):
     return units_per_rank * world / elapsed
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv: list[str]) -> int:
+    """`bench.py --gpus N` started without a torch.distributed environment: start N rank
+    processes of this script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR 127.0.0.1 /
+    MASTER_PORT set, one rank per GPU), wait for all, and return the worst exit code.  The
+    parent never touches the GPU (no torch.cuda call: it only forks children), so the
+    children own the devices; rank 0 prints the JSON line."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
+def check_world(args, world: int):
+    """Every rank: the job must be the one asked for (`--gpus N` = N ranks), and with RCCL
+    every rank needs its own GPU.  A mismatch exits non-zero instead of timing the wrong job."""
+    if world != args.gpus:
+        sys.stderr.write(f"bench.py: WORLD_SIZE {world} != --gpus {args.gpus}\n")
+        sys.exit(2)
+    if args.dist_backend == "nccl" and args.stub_step_ms is None:
+        import torch
+        if torch.cuda.device_count() < world:
+            sys.stderr.write(f"bench.py: {world} ranks need {world} GPUs, "
+                             f"{torch.cuda.device_count()} visible\n")
+            sys.exit(2)
+
+
+def stub_main(args, world, rank, dist):
+    """Test hook (`--stub-step-ms`): the launcher and the timing protocol with a CPU sleep in
+    place of the engine step (no GPU).  Never a measurement: `data` says "stub"."""
+    lanes = CONFIGS[args.config]["n_lanes"]
+    elapsed = timed_steps(lambda: time.sleep(args.stub_step_ms * 1e-3 * (1 + 0.5 * rank)),
+                          args.steps, args.warmup, dist, device="cpu")
+    if rank == 0:
+        print(json.dumps({"metric": "Leduc self-play hands/sec", "unit": "hands/s",
+                          "value": job_value(args.steps * lanes, world, elapsed), "n_gpus": world,
+                          "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": elapsed / args.steps * 1e3, "data": "stub",
+                          "config": {"parallelism": f"dp{world}"}}), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -192,7 +254,16 @@ def main():
     ap.add_argument("--ar-allreduce", default="auto", choices=["auto", "on", "off"],
                     help="all-reduce of the AR (average-policy) gradient steps once per engine "
                          "step over the ranks (C4; shards.AvgPolicyAllReduce); auto = on for N > 1")
+    ap.add_argument("--stub-step-ms", type=float, default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # the driver's `bench.py --gpus N` without torch.distributed.run: one rank per GPU
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    check_world(args, int(os.environ.get("WORLD_SIZE", "1")))
+    if args.stub_step_ms is not None:
+        world, rank, _, dist = init_dist("gloo")
+        return stub_main(args, world, rank, dist)
 
     import torch
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -217,22 +288,28 @@ def main():
         eng.step()
         if avg is not None:
             avg()
+    dev = "cuda" if args.dist_backend == "nccl" else "cpu"
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    # `value`: K steps with no instrumentation at all
     s0 = eng.stats()
+    elapsed = timed_steps(step, args.steps, 0, dist, torch.cuda.synchronize, device=dev)
+    s1 = eng.stats()
+    # per-kernel durations: K more steps with HIP events around every launch (kernel_ms,
+    # roofline); their wall time is reported beside `value`, never as it
     eng.set_timing(True)
     eng.timings()
-    elapsed = timed_steps(step, args.steps, 0, dist, torch.cuda.synchronize,
-                          device="cuda" if args.dist_backend == "nccl" else "cpu")
+    elapsed_ev = timed_steps(step, args.steps, 0, dist, torch.cuda.synchronize, device=dev)
     timings = eng.timings()
-    s1 = eng.stats()
+    eng.set_timing(False)
+    s2 = eng.stats()
 
     hands_rank = args.steps * cfg["n_lanes"]
     value = job_value(hands_rank, world, elapsed)
-    br_upd = sum(s1["br_updates"]) - sum(s0["br_updates"])
-    ar_upd = sum(s1["ar_updates"]) - sum(s0["ar_updates"])
-    rl_ins = sum(s1["rl_total"]) - sum(s0["rl_total"])
+    br_upd = sum(s2["br_updates"]) - sum(s1["br_updates"])      # the instrumented pass's work
+    ar_upd = sum(s2["ar_updates"]) - sum(s1["ar_updates"])
+    rl_ins = sum(s1["rl_total"]) - sum(s0["rl_total"])          # the timed pass's inserts
     sl_ins = sum(s1["sl_total"]) - sum(s0["sl_total"])
     k_ms = {k: v[0] / max(v[1], 1) for k, v in timings.items()}
     k_launches = {k: v[1] for k, v in timings.items()}
@@ -244,6 +321,13 @@ def main():
                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "traffic": None,
                     "bytes_per_hand": bytes_hand, "avg_ms": k_ms["k_rollout"]}
     roof_rollout["frac"] = roof_rollout["achieved"] / PEAK_HBM_GBS
+    # SURVEY 8(d)'s whole-path figure: rollout writes + the sampled reads at the reference
+    # cadence (T_rl / 128 updates x 128 rows x (257 + 132) B) per hand, over the timed step
+    step_bytes_hand = bytes_hand + (t_rl / 128.0) * 128 * (BYTES_RL + BYTES_SL)
+    whole_step = {"bound": "hbm", "unit": "GB/s", "peak": PEAK_HBM_GBS,
+                  "bytes_per_hand": step_bytes_hand,
+                  "achieved": step_bytes_hand * hands_rank / (elapsed / 1.0) / 1e9}
+    whole_step["frac"] = whole_step["achieved"] / PEAK_HBM_GBS
 
     def chain_roof(name, updates):
         n = max(k_launches[name], 1)
@@ -277,19 +361,23 @@ def main():
         return {"kernel": name, "bound": "issue", "achieved": issue, "peak": measured,
                 "unit": "cycles per SGD step (static issue / measured)", "frac": issue / measured,
                 "us_per_step": k_ms[name] * 1e3 / steps, "source": "profiles/r01_chain_census.json"}
-    roofs = {"k_chain3_br": chain_roof("k_chain3_br", br_upd),
-             "k_chain3_ar": chain_roof("k_chain3_ar", ar_upd),
-             "k_rollout": roof_rollout,
-             "k_chain3_br_hbm": chain_roof_hbm("k_chain3_br", br_upd, BYTES_RL),
+    # roofline: SURVEY 8(d)'s HBM framing (the judged bound) of each kernel; the MFMA and
+    # issue framings of the chains go to roofline_other
+    roofs = {"k_chain3_br_hbm": chain_roof_hbm("k_chain3_br", br_upd, BYTES_RL),
+             "k_chain3_ar_hbm": chain_roof_hbm("k_chain3_ar", ar_upd, BYTES_SL),
+             "k_rollout_hbm": roof_rollout,
+             "k_chain3_br_mfma": chain_roof("k_chain3_br", br_upd),
+             "k_chain3_ar_mfma": chain_roof("k_chain3_ar", ar_upd),
              "k_chain3_br_issue": chain_issue("k_chain3_br", br_upd, "br"),
              # one AR launch runs both agents' chains side by side: it lasts as long as the
              # agent with more updates
-             "k_chain3_ar_issue": chain_issue("k_chain3_ar", max(s1["ar_updates"][a] - s0["ar_updates"][a]
+             "k_chain3_ar_issue": chain_issue("k_chain3_ar", max(s2["ar_updates"][a] - s1["ar_updates"][a]
                                                                  for a in (0, 1)), "ar")}
     # the dominant kernel = largest GPU time inside the timed region
-    singles = [k for k in timings if k != "learner"]
+    singles = [k for k in timings if k not in ("learner", "learner_prep")]
     dom = max(singles, key=lambda k: timings[k][0])
-    roofline = dict(roofs.get(dom, roof_rollout))
+    roof_key = f"{dom}_hbm" if f"{dom}_hbm" in roofs else "k_rollout_hbm"
+    roofline = dict(roofs[roof_key])
     pmc = load_pmc(args.config, roofline["kernel"])
     if pmc is not None:
         roofline["traffic"] = pmc
@@ -303,6 +391,7 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
+        "ms_per_step_event_timed": elapsed_ev / args.steps * 1e3,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -313,13 +402,14 @@ def main():
                    "inserts_per_update": 128, "batch": 128, "parallelism": (f"dp{world}: shards + AR-gradient all-reduce per engine step"
                                    if avg is not None else f"replicas x{world}")},
         "roofline": roofline,
-        "roofline_other": {k: v for k, v in roofs.items() if k != roofline["kernel"]},   # incl. the
-        # dominant chain's HBM framing (k_chain3_br_hbm: SURVEY 8(d) bytes, PMC traffic)
+        "roofline_other": {k: v for k, v in roofs.items() if k != roof_key},
+        "whole_step_hbm_per_gpu": whole_step,
         "kernel_ms": k_ms,
+        "kernel_ms_source": "HIP events around every launch, second pass of K steps",
         "rollout_only_hands_per_s": cfg["n_lanes"] / (rollout_path_ms * 1e-3) * world,
         "per_step": {"br_updates": br_upd / args.steps, "ar_updates": ar_upd / args.steps,
                      "rl_inserts_per_hand": t_rl, "sl_inserts_per_hand": t_sl},
-        "exploitability_proxy": sum(s1["exploitability"]),
+        "exploitability_proxy": sum(s2["exploitability"]),
     }
     if avg is not None:
         out["ar_allreduce"] = {"calls": avg.calls, "bytes_per_call": 4 * avg.flat.numel(),
@@ -328,7 +418,7 @@ def main():
     ex = {m: eng.exploitability(m) for m in (0, 1)}
     out["exploitability_exact"] = {
         "softmax_mixed": ex[0]["exploitability"], "argmax_as_executed": ex[1]["exploitability"],
-        "hands_trained_per_gpu": int(s1["hands"]), "unit": "chips (BR_0 + BR_1)"}
+        "hands_trained_per_gpu": int(s2["hands"]), "unit": "chips (BR_0 + BR_1)"}
     if rank == 0 and world == 1 and not args.no_cpu:
         threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, threads, cfg)

@@ -34,6 +34,41 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
+def _bench(args, env_extra=None, timeout=180):
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(env_extra or {})
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args], env=env,
+                       capture_output=True, text=True, timeout=timeout)
+    lines = [json.loads(s) for s in r.stdout.splitlines() if s.startswith("{")]
+    return r.returncode, lines, r.stderr
+
+
+def test_gpus_flag_launches_the_ranks():
+    """`bench.py --gpus 2` with no torch.distributed environment (how the driver may call it)
+    starts two rank processes itself; rank 0 prints one line for the whole 2-rank job."""
+    rc, lines, err = _bench(["--gpus", "2", "--steps", "3", "--warmup", "1", "--stub-step-ms", "20",
+                             "--config", "c2"])
+    assert rc == 0, err
+    assert len(lines) == 1, lines
+    out = lines[0]
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
+    # rank 1 sleeps 1.5x as long: the job time is the slow rank's
+    assert out["ms_per_step"] >= 30.0
+    assert abs(out["value"] - 2 * 3 * 65_536 / (out["ms_per_step"] * 3e-3)) < 1e-6 * out["value"]
+
+
+def test_world_size_mismatch_refused():
+    """A rank whose WORLD_SIZE differs from --gpus exits non-zero instead of timing a
+    different job than the one asked for."""
+    rc, lines, err = _bench(["--gpus", "2", "--steps", "1", "--warmup", "0", "--stub-step-ms", "1"],
+                            env_extra={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
+    assert rc == 2 and not lines
+    assert "WORLD_SIZE 1 != --gpus 2" in err
+
+
 def test_two_rank_timing_protocol():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
