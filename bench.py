@@ -62,6 +62,15 @@ CONFIGS = {
                   label="C3's memories and cadence at 4,096 lanes (policy lag 4k hands; DESIGN §9)"),
     "c3_64k": dict(n_lanes=65_536, rl_capacity=200_000, sl_capacity=2_000_000,
                    label="C3's memories and cadence at 65,536 lanes (policy lag 64k hands; DESIGN §9)"),
+    # engine groups (nfsp_group_*): C3's 1,048,576 lanes per GPU as R learner replicas of
+    # 1M / R lanes, each with C3's own memories (M_RL 200k, M_SL 2M) and cadence, their SGD
+    # chains in shared launches, and the AR nets averaged over the replicas after every step
+    # (C4's exchange, on device).  A new measured configuration beside C3, not C3 itself.
+    **{f"c3_r{R}": dict(n_lanes=1_048_576, replicas=R, rl_capacity=200_000, sl_capacity=2_000_000,
+                        label=f"C3 as {R} learner replicas x {1_048_576 // R:,} Leduc lanes on one GPU, "
+                              f"each with device M_RL 200k + M_SL 2M, target sync 150, reference cadence; "
+                              f"AR nets averaged over the replicas every step")
+       for R in (2, 4, 8, 16, 32, 64)},
     "c5": dict(n_lanes=1_048_576, rl_capacity=200_000, sl_capacity=2_000_000, game="kuhn",
                label="C5: Kuhn swap-in, 1,048,576 lanes/GPU, C3's memories and cadence"),
 }
@@ -274,11 +283,17 @@ def main():
     pkg = __graft_entry__.load_package()
     cfg = CONFIGS[args.config]
     game = pkg.native.GAME_KUHN if cfg.get("game") == "kuhn" else pkg.native.GAME_LEDUC
-    eng = pkg.engine.SelfPlayEngine(n_lanes=cfg["n_lanes"], rl_capacity=cfg["rl_capacity"],
-                                    sl_capacity=cfg["sl_capacity"], seed=1234 + rank,
-                                    init_seed=rank, game=game)
+    R = cfg.get("replicas", 1)
+    if R > 1:        # seeds 1234 + R rank + r: distinct over every replica of the job
+        eng = pkg.engine.EngineGroup(R, n_lanes=cfg["n_lanes"] // R, rl_capacity=cfg["rl_capacity"],
+                                     sl_capacity=cfg["sl_capacity"], seed=1234 + R * rank,
+                                     init_seed=R * rank, game=game, avg_ar=True)
+    else:
+        eng = pkg.engine.SelfPlayEngine(n_lanes=cfg["n_lanes"], rl_capacity=cfg["rl_capacity"],
+                                        sl_capacity=cfg["sl_capacity"], seed=1234 + rank,
+                                        init_seed=rank, game=game)
     avg = None
-    if dist is not None and (args.ar_allreduce == "on" or (args.ar_allreduce == "auto" and world > 1)):
+    if R == 1 and dist is not None and (args.ar_allreduce == "on" or (args.ar_allreduce == "auto" and world > 1)):
         # C4: the AR nets of both agents, averaged over the ranks once per engine step
         avg = pkg.shards.AvgPolicyAllReduce(
             [eng.weights_tensor(a, pkg.engine.NET_AR) for a in (0, 1)], dist,
@@ -312,10 +327,11 @@ def main():
     rl_ins = sum(s1["rl_total"]) - sum(s0["rl_total"])          # the timed pass's inserts
     sl_ins = sum(s1["sl_total"]) - sum(s0["sl_total"])
     k_ms = {k: v[0] / max(v[1], 1) for k, v in timings.items()}
+    k_step_ms = {k: v[0] / args.steps for k, v in timings.items()}       # per engine step
     k_launches = {k: v[1] for k, v in timings.items()}
     t_rl, t_sl = rl_ins / hands_rank, sl_ins / hands_rank
     bytes_hand = BYTES_RL * t_rl + BYTES_SL * t_sl
-    rollout_bytes = bytes_hand * cfg["n_lanes"]
+    rollout_bytes = bytes_hand * cfg["n_lanes"] / R                       # per launch
     roof_rollout = {"kernel": "k_rollout", "bound": "hbm",
                     "achieved": rollout_bytes / (k_ms["k_rollout"] * 1e-3) / 1e9,
                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "traffic": None,
@@ -351,8 +367,8 @@ def main():
         costs) against the measured cycles per step at the chain's effective clock (2.40 GHz,
         tools/chain_clock.py).  frac = the share of the step one wave spends issuing."""
         path = os.path.join(REPO, "profiles", "r01_chain_census.json")
-        n = max(k_launches[name], 1)
-        steps = updates * 2 * 128 / 32 / n                  # epochs x minibatches per launch
+        n = max(k_launches[name], 1) * (par if name == "k_chain3_br" else 1)
+        steps = updates * 2 * 128 / 32 / n                  # epochs x minibatches per workgroup
         if not os.path.exists(path) or steps <= 0:
             return None
         with open(path) as f:
@@ -361,6 +377,11 @@ def main():
         return {"kernel": name, "bound": "issue", "achieved": issue, "peak": measured,
                 "unit": "cycles per SGD step (static issue / measured)", "frac": issue / measured,
                 "us_per_step": k_ms[name] * 1e3 / steps, "source": "profiles/r01_chain_census.json"}
+    # the issue framing is per chain workgroup: the AR launch lasts as long as its longest
+    # chain, a BR launch runs up to 2R segments side by side
+    reps1, reps2 = s1.get("replicas", [s1]), s2.get("replicas", [s2])
+    ar_max = max(b["ar_updates"][a] - x["ar_updates"][a] for x, b in zip(reps1, reps2) for a in (0, 1))
+    par = 2 * R if R > 1 else 1
     # roofline: SURVEY 8(d)'s HBM framing (the judged bound) of each kernel; the MFMA and
     # issue framings of the chains go to roofline_other
     roofs = {"k_chain3_br_hbm": chain_roof_hbm("k_chain3_br", br_upd, BYTES_RL),
@@ -371,8 +392,7 @@ def main():
              "k_chain3_br_issue": chain_issue("k_chain3_br", br_upd, "br"),
              # one AR launch runs both agents' chains side by side: it lasts as long as the
              # agent with more updates
-             "k_chain3_ar_issue": chain_issue("k_chain3_ar", max(s2["ar_updates"][a] - s1["ar_updates"][a]
-                                                                 for a in (0, 1)), "ar")}
+             "k_chain3_ar_issue": chain_issue("k_chain3_ar", ar_max, "ar")}
     # the dominant kernel = largest GPU time inside the timed region
     singles = [k for k in timings if k not in ("learner", "learner_prep")]
     dom = max(singles, key=lambda k: timings[k][0])
@@ -382,7 +402,7 @@ def main():
     if pmc is not None:
         roofline["traffic"] = pmc
         roofline["traffic_source"] = f"profiles/pmc_{args.config}.json (rocprofv3 --pmc passes)"
-    rollout_path_ms = k_ms["k_rollout"] + k_ms["k_scan"] + k_ms["k_commit"]
+    rollout_path_ms = k_step_ms["k_rollout"] + k_step_ms["k_scan"] + k_step_ms["k_commit"]
     out = {
         "metric": "Kuhn self-play hands/sec" if cfg.get("game") == "kuhn" else "Leduc self-play hands/sec",
         "value": value,
@@ -397,14 +417,17 @@ def main():
         "vs_baseline": None,
         "dtype": "fp32",
         "data": "synthetic: Philox self-play deals/draws, Glorot-uniform random-init nets",
-        "config": {"workload": cfg["label"], "lanes_per_gpu": cfg["n_lanes"],
+        "config": {"workload": cfg["label"], "lanes_per_gpu": cfg["n_lanes"], "learner_replicas_per_gpu": R,
                    "rl_capacity": cfg["rl_capacity"], "sl_capacity": cfg["sl_capacity"],
                    "inserts_per_update": 128, "batch": 128, "parallelism": (f"dp{world}: shards + AR-gradient all-reduce per engine step"
-                                   if avg is not None else f"replicas x{world}")},
+                                   if avg is not None else
+                                   f"replicas x{world} GPUs x {R} learner replicas per GPU (on-device AR average per step)"
+                                   if R > 1 else f"replicas x{world}")},
         "roofline": roofline,
         "roofline_other": {k: v for k, v in roofs.items() if k != roof_key},
         "whole_step_hbm_per_gpu": whole_step,
         "kernel_ms": k_ms,
+        "kernel_ms_per_step": k_step_ms,
         "kernel_ms_source": "HIP events around every launch, second pass of K steps",
         "rollout_only_hands_per_s": cfg["n_lanes"] / (rollout_path_ms * 1e-3) * world,
         "per_step": {"br_updates": br_upd / args.steps, "ar_updates": ar_upd / args.steps,

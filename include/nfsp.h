@@ -207,7 +207,7 @@ typedef struct nfsp_engine_cfg {
   int32_t n_lanes;             /* hands in flight */
   int32_t hidden;              /* [Agent] HiddenLayer, must be 64 */
   int64_t rl_capacity;         /* M_RL size (reference: [Utils] Buffersize 40000) */
-  int64_t sl_capacity;         /* M_SL size (reference: 40000) */
+  int64_t sl_capacity;         /* M_SL size (reference: 40000); < 2^31 */
   int32_t batch;               /* [Agent] MiniBatchSize 128 */
   int32_t inserts_per_update;  /* 128: game_step % 128 (agent/agent.py:153) */
   int32_t target_every;        /* [Agent] TargetModelUpdateRate 150 */
@@ -284,6 +284,37 @@ int nfsp_engine_last_update(nfsp_engine* e, int agent, int role, int64_t** dev_r
  * hand).  Their exclusive prefix over lanes is each lane's first record in the canonical
  * insert order (lane, then play order) -- how a test finds one lane's records in M_RL. */
 int nfsp_engine_lane_counts(nfsp_engine* e, uint32_t** dev_counts);
+
+/* ---- engine groups: several learners on one GPU ----
+ * A group holds R replicas of the engine.  Each replica is an independent
+ * main.train (main.py:21-75) over cfg.n_lanes lanes: its own hands, its own M_RL / M_SL, and
+ * its own nets.  Replica r uses cfg.seed + r, and is bit-identical to a standalone engine
+ * created with that seed and stepped as often.  nfsp_group_step does rollout + update for
+ * every replica.  The SGD chains of all replicas run in shared launches: one AR launch of 2R
+ * workgroups; the BR chains in rounds, where round k holds every (replica, agent)'s k-th
+ * target-sync segment.  A chain workgroup occupies one CU, so one learner pair's 4 CUs
+ * become 4R.  This is BASELINE C4's shard model inside one GPU.
+ * With NFSP_GROUP_AVG_AR, replica 0's AR nets are first copied to every replica.  After every
+ * step, each AR net becomes W0 + sum_r (W_r - W0) / R, with W0 = the nets after the
+ * previous exchange.  This is shards.AvgPolicyAllReduce's per-step exchange, done on device.
+ * A replica's handle (nfsp_group_engine) serves weights, stats, memories, the loss log and
+ * timing; nfsp_engine_update / nfsp_engine_step on it are refused. */
+typedef struct nfsp_group nfsp_group;
+#define NFSP_GROUP_MAX_REPLICAS 64
+#define NFSP_GROUP_AVG_AR 1u
+int nfsp_group_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, int replicas, unsigned flags,
+                      nfsp_group** out);
+int nfsp_group_destroy(nfsp_group* g);
+int nfsp_group_engine(nfsp_group* g, int replica, nfsp_engine** out);
+int nfsp_group_step(nfsp_group* g);
+/* The AR exchange by itself (nfsp_group_step does it when NFSP_GROUP_AVG_AR is set).  Its
+ * first call copies replica 0's AR nets everywhere. */
+int nfsp_group_average_ar(nfsp_group* g);
+int nfsp_group_set_timing(nfsp_group* g, int on);
+/* nfsp_engine_get_timings summed over the replicas.  The shared chain and target launches
+ * count once each. */
+int nfsp_group_get_timings(nfsp_group* g, double* ms /*[8]*/, int64_t* launches /*[8]*/);
+int nfsp_group_rounds(nfsp_group* g, int64_t* out);   /* BR rounds of the last learner call */
 
 /* ---- evaluation ----
  * Exact exploitability of two average-policy nets (packed weights, device pointers; e.g.

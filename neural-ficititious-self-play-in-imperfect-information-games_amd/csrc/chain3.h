@@ -16,18 +16,21 @@ using namespace nfsp::eng;
 // back with the whole net in registers (k_chain3).  Reference: agent/agent.py:241-264
 // (model.fit(batch_size=32, epochs=2) of the BR Q-net and the AR policy net).
 // ---------------------------------------------------------------------------
-struct ChainArgs {
-  float* w[2];                    // weights of (agent, net)
-  float* sync_to[2];              // BR: target net to copy into at the end (or null)
-  const StepRec* rec;             // [2][umax][E][B / 32] step records (prep kernels)
+// One chain workgroup's work: a net's weights and the step records of one (engine, agent).
+struct ChainJob {
+  float* w;                       // weights of (agent, net)
+  float* sync_to;                 // BR: target net to copy into at the end (or null)
+  const StepRec* rec;             // this agent's step records [umax][E][B / 32] (prep kernels)
   const uint8_t* active;          // AR: per-update flag, 0..0 1..1 in u (null for BR)
-  int64_t umax;
-  int64_t u0[2], u1[2];           // update range per agent
-  int agents[2];                  // blockIdx -> agent
+  float* loss_out;                // optional: [umax][E] Keras epoch losses (the values the
+                                  // reference's TensorBoard callbacks log, agent/agent.py:84-88)
+  int64_t u0, u1;                 // update range
+};
+struct ChainArgs {
+  ChainJob job[2];                // blockIdx -> job (one engine: <= 2 workgroups)
+  const ChainJob* jobs;           // device table instead, when set (engine groups: 2R workgroups)
   int B, E;
   unsigned long long* stamps;     // diagnostic build only (NFSP_CHAIN_STAMPS): phase cycles
-  float* loss_out;                // optional: [2][umax][E] Keras epoch losses (the values the
-                                  // reference's TensorBoard callbacks log, agent/agent.py:84-88)
 };
 
 // In-kernel phase stamps (cdna_hip_programming.md §7): a separate diagnostic build only.
@@ -169,18 +172,21 @@ __device__ inline floatx4 mfma3t(bf16x8 ahi, bf16x8 amid, bf16x8 alo, bf16x8 b) 
 
 // RELU: 0 = the AR net (softmax, categorical cross-entropy), 1 = the BR net (ReLU Q head,
 // Huber), 2 = a BR net with a linear Q head (NFSP_EXT_LINEAR_Q, Huber).
-template <int RELU, int LOSS>
+// TABLE: the workgroups' jobs come from the device table C.jobs (engine groups); else from
+// the kernel arguments (C.job, one engine) -- a separate instantiation, so the one-engine
+// chain's code is not touched by the group's
+template <int RELU, int LOSS, int TABLE = 0>
 __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   Chain3Smem& sm = *reinterpret_cast<Chain3Smem*>(smem_raw);
-  const int a = C.agents[blockIdx.x];
+  const ChainJob J = TABLE ? C.jobs[blockIdx.x] : C.job[blockIdx.x];
   const int tid = threadIdx.x;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l = tid & 63;
   const int g = l >> 4, c = l & 15;
   const int hid = 16 * w + c;
   const int sl = 16 * (g >> 1) + c;            // this lane's loss sample
-  float* gw = C.w[blockIdx.x];
+  float* gw = J.w;
   float wr[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -193,13 +199,12 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
   const int spu = C.E * nmb;                   // SGD steps per update
   const float inv3m = 1.0f / (float)(3 * CHAIN_MB);
   const float invm = 1.0f / (float)CHAIN_MB;
-  const int64_t slot0 = (int64_t)a * C.umax;
-  const int64_t u1 = C.u1[blockIdx.x];
-  int64_t u0 = C.u0[blockIdx.x];
-  if (C.active) {          // AR: skip the inactive prefix (M_SL <= batch; monotone in u)
+  const int64_t u1 = J.u1;
+  int64_t u0 = J.u0;
+  if (J.active) {          // AR: skip the inactive prefix (M_SL <= batch; monotone in u)
     while (u0 < u1) {
       const int64_t q = u0 + l;
-      const unsigned long long m = __ballot(q < u1 && C.active[slot0 + q]);
+      const unsigned long long m = __ballot(q < u1 && J.active[q]);
       if (m) { u0 += __builtin_ctzll(m); break; }
       u0 += 64;
     }
@@ -207,7 +212,7 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
   }
   const int T1 = (int)(u1 * spu);
   int t = (int)(u0 * spu);
-  const uint4* recb = reinterpret_cast<const uint4*>(C.rec + slot0 * spu);
+  const uint4* recb = reinterpret_cast<const uint4*>(J.rec);
   // this wave's quarter of record p (clamped), into two registers / back into ring slot p & 3;
   // the lanes past the quarter load a duplicate chunk and store it to the sink
   const bool in_q = l < REC_QUARTER - 64;
@@ -370,7 +375,7 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
         loss_acc += x * invm;
         if (in_u % nmb == nmb - 1) {
           const int64_t uu = t / spu, ee = in_u / nmb;
-          C.loss_out[(slot0 + uu) * C.E + ee] = loss_acc / (float)nmb;
+          J.loss_out[uu * C.E + ee] = loss_acc / (float)nmb;
           loss_acc = 0.f;
         }
       }
@@ -466,7 +471,7 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
     }
   }
 #endif
-  float* dsts[2] = {gw, C.sync_to[blockIdx.x]};
+  float* dsts[2] = {gw, J.sync_to};
   for (int k = 0; k < 2; ++k) {
     float* dst = dsts[k];
     if (!dst) continue;
@@ -492,21 +497,40 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
 
 // The chains' dynamic-LDS attribute (CHAIN_LDS), set once per device and kernel pair
 // (`mask`: one bit per device, kept by the caller's translation unit).
-inline int set_chain_lds(std::atomic<uint64_t>& mask, const void* f0, const void* f1) {
+inline int set_chain_lds(std::atomic<uint64_t>& mask, const void* f0, const void* f1, const void* f2,
+                         const void* f3) {
   int dev = 0;
   NFSP_HIP(hipGetDevice(&dev));
   const uint64_t bit = 1ull << (dev & 63);
   if (mask.load(std::memory_order_acquire) & bit) return NFSP_OK;
-  for (const void* f : {f0, f1})
+  for (const void* f : {f0, f1, f2, f3})
     NFSP_HIP(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, CHAIN_LDS));
   mask.fetch_or(bit, std::memory_order_acq_rel);
   return NFSP_OK;
 }
 
-// AR chain launcher (chain_ar.hip): k_chain3<0, loss_log> on `s`, `blocks` workgroups.
+// Launch k_chain3<RELU, loss_log, C.jobs != null> on `s` with `blocks` workgroups (after
+// setting the LDS attribute of the four instantiations once per device).
+template <int RELU>
+int launch_chain(const ChainArgs& C, int blocks, bool loss_log, hipStream_t s, std::atomic<uint64_t>& attr) {
+  const int rc = set_chain_lds(attr, (const void*)k_chain3<RELU, 0, 0>, (const void*)k_chain3<RELU, 1, 0>,
+                               (const void*)k_chain3<RELU, 0, 1>, (const void*)k_chain3<RELU, 1, 1>);
+  if (rc != NFSP_OK) return rc;
+  if (C.jobs) {
+    if (loss_log) k_chain3<RELU, 1, 1><<<blocks, 256, CHAIN_LDS, s>>>(C);
+    else k_chain3<RELU, 0, 1><<<blocks, 256, CHAIN_LDS, s>>>(C);
+  } else {
+    if (loss_log) k_chain3<RELU, 1, 0><<<blocks, 256, CHAIN_LDS, s>>>(C);
+    else k_chain3<RELU, 0, 0><<<blocks, 256, CHAIN_LDS, s>>>(C);
+  }
+  NFSP_LAUNCHED("k_chain3");
+  return NFSP_OK;
+}
+
+// AR chain launcher (chain_ar.hip): k_chain3<0, loss_log, *> on `s`, `blocks` workgroups.
 int launch_chain_ar(const ChainArgs& C, int blocks, bool loss_log, hipStream_t s);
 // BR chain with a linear Q head (NFSP_EXT_LINEAR_Q; chain_brlin.hip): k_chain3<2, loss_log>.
-int launch_chain_br_linear(const ChainArgs& C, bool loss_log, hipStream_t s);
+int launch_chain_br_linear(const ChainArgs& C, int blocks, bool loss_log, hipStream_t s);
 
 }  // namespace chain
 }  // namespace nfsp

@@ -9,12 +9,7 @@ namespace chain {
 
 int launch_chain_ar(const ChainArgs& C, int blocks, bool loss_log, hipStream_t s) {
   static std::atomic<uint64_t> attr{0};
-  const int rc = set_chain_lds(attr, (const void*)k_chain3<0, 0>, (const void*)k_chain3<0, 1>);
-  if (rc != NFSP_OK) return rc;
-  if (loss_log) k_chain3<0, 1><<<blocks, 256, CHAIN_LDS, s>>>(C);
-  else k_chain3<0, 0><<<blocks, 256, CHAIN_LDS, s>>>(C);
-  NFSP_LAUNCHED("k_chain(AR)");
-  return NFSP_OK;
+  return launch_chain<0>(C, blocks, loss_log, s, attr);
 }
 
 }  // namespace chain

@@ -7,14 +7,9 @@
 namespace nfsp {
 namespace chain {
 
-int launch_chain_br_linear(const ChainArgs& C, bool loss_log, hipStream_t s) {
+int launch_chain_br_linear(const ChainArgs& C, int blocks, bool loss_log, hipStream_t s) {
   static std::atomic<uint64_t> attr{0};
-  const int rc = set_chain_lds(attr, (const void*)k_chain3<2, 0>, (const void*)k_chain3<2, 1>);
-  if (rc != NFSP_OK) return rc;
-  if (loss_log) k_chain3<2, 1><<<1, 256, CHAIN_LDS, s>>>(C);
-  else k_chain3<2, 0><<<1, 256, CHAIN_LDS, s>>>(C);
-  NFSP_LAUNCHED("k_chain(BR, linear)");
-  return NFSP_OK;
+  return launch_chain<2>(C, blocks, loss_log, s, attr);
 }
 
 }  // namespace chain

@@ -434,7 +434,11 @@ extern "C" int nfsp_engine_destroy(nfsp_engine* e) {
   return NFSP_OK;
 }
 
-extern "C" int nfsp_engine_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, nfsp_engine** out) {
+namespace nfsp {
+namespace eng {
+// own_streams: the engine's own AR / BR chain streams (nfsp_engine_update); a replica of an
+// engine group has none (the group launches its chains)
+int engine_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, bool own_streams, nfsp_engine** out) {
   NFSP_REQUIRE(ctx && cfg && out, "null argument");
   NFSP_REQUIRE(cfg->hidden == nn::H, "only hidden == 64 is built");
   NFSP_REQUIRE(cfg->n_lanes > 0 && cfg->n_lanes < (1 << 24), "n_lanes must be in [1, 2^24)");
@@ -444,7 +448,9 @@ extern "C" int nfsp_engine_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, nfs
   NFSP_REQUIRE(cfg->epochs >= 1 && cfg->epochs <= 4, "epochs must be in [1, 4]");
   NFSP_REQUIRE(cfg->rl_capacity > cfg->batch && cfg->sl_capacity > cfg->batch,
                "capacities must exceed the batch");
-  NFSP_REQUIRE(cfg->sl_capacity < (1ll << 40) && cfg->rl_capacity < (1ll << 40), "capacity too large");
+  // reservoir slots are int32 in the learner (LearnBufs::res_slot)
+  NFSP_REQUIRE(cfg->sl_capacity < (1ll << 31), "sl_capacity must be < 2^31");
+  NFSP_REQUIRE(cfg->rl_capacity < (1ll << 40), "rl_capacity too large");
   NFSP_REQUIRE(cfg->inserts_per_update >= 1 && cfg->target_every >= 1, "bad cadence");
   NFSP_REQUIRE((cfg->quirks & ~(NFSP_QUIRKS_REFERENCE | NFSP_TEXTBOOK)) == 0,
                "unknown bits in quirks (NFSP_QUIRK_* | NFSP_EXT_*)");
@@ -498,6 +504,7 @@ extern "C" int nfsp_engine_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, nfs
   EALLOC(L.res_next, 4 * pc);
   EALLOC(L.res_slot, 4 * pc);
   for (hipStream_t* st : {&e->s_br[0], &e->s_br[1], &e->s_ar}) {
+    if (!own_streams) break;
     hipError_t sr = hipStreamCreateWithFlags(st, hipStreamNonBlocking);
     if (sr != hipSuccess) {
       nfsp_engine_destroy(e);
@@ -519,6 +526,12 @@ extern "C" int nfsp_engine_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, nfs
   *out = e;
   return NFSP_OK;
 }
+}  // namespace eng
+}  // namespace nfsp
+
+extern "C" int nfsp_engine_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, nfsp_engine** out) {
+  return nfsp::eng::engine_create(ctx, cfg, true, out);
+}
 
 extern "C" int nfsp_engine_weights(nfsp_engine* e, int agent, int net, float** dev_w) {
   NFSP_REQUIRE(e && dev_w, "null argument");
@@ -527,8 +540,9 @@ extern "C" int nfsp_engine_weights(nfsp_engine* e, int agent, int net, float** d
   return NFSP_OK;
 }
 
-extern "C" int nfsp_rollout(nfsp_engine* e) {
-  NFSP_REQUIRE(e, "null argument");
+namespace nfsp {
+namespace eng {
+int rollout_launch(nfsp_engine* e) {
   NFSP_REQUIRE(!e->pending_update, "nfsp_engine_update must consume the previous rollout first");
   hipStream_t s = e->ctx->stream;
   RolloutArgs A;
@@ -564,6 +578,14 @@ extern "C" int nfsp_rollout(nfsp_engine* e) {
   e->rollouts++;
   e->pending_update = true;
   return NFSP_OK;
+}
+}  // namespace eng
+}  // namespace nfsp
+
+extern "C" int nfsp_rollout(nfsp_engine* e) {
+  NFSP_REQUIRE(e, "null argument");
+  NFSP_REQUIRE(e->s_ar, "a replica of an engine group is stepped by nfsp_group_step");
+  return nfsp::eng::rollout_launch(e);
 }
 
 extern "C" int nfsp_engine_step(nfsp_engine* e) {

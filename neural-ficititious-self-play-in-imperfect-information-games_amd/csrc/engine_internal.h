@@ -229,6 +229,8 @@ namespace nfsp {
 namespace eng {
 
 hipEvent_t take_event(nfsp_engine* e);
+int engine_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, bool own_streams, nfsp_engine** out);
+int rollout_launch(nfsp_engine* e);   // nfsp_rollout's launches (also the group's, per replica)
 
 // RAII bracket: records start/stop events around launches on `stream` when timing is on
 struct KTimer {

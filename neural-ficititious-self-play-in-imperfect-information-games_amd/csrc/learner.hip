@@ -20,6 +20,7 @@
 // the AR chains run on separate streams.
 #include <math.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "engine_internal.h"
 #include "chain3.h"
@@ -281,9 +282,22 @@ __global__ void __launch_bounds__(256) k_res_apply(PrepArgs P) {
 // ---------------------------------------------------------------------------
 // DQN targets of one BR segment (agent/agent.py:219-241), one update per workgroup
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_br_targets(LearnBufs LB, const float* __restrict__ tw, int a,
-                                                    int64_t u0, int B, int E, double gamma,
-                                                    unsigned quirks, int64_t it0, double lr0) {
+// One (engine, agent) segment: the agent's learner buffers (update u of the learner call at
+// index u), the target net, and the segment's update range [u0, u0 + n).
+struct TargetJob {
+  const BrRow* rows;   // [umax][B]
+  const uint8_t* perm; // [umax][E][B]
+  double* expl;        // [umax]
+  StepRec* rec;        // [umax][E][B / 32]
+  const float* tw;     // target net
+  int64_t u0, n;
+  int64_t it0;         // the agent's iteration count before the learner call
+};
+
+// blockIdx.x = update within the segment; blockIdx.y = job (of `jobs`, else `one`)
+__global__ void __launch_bounds__(256) k_br_targets(const TargetJob* __restrict__ jobs, TargetJob one,
+                                                    int B, int E, double gamma, unsigned quirks,
+                                                    double lr0) {
   // threads 0..127: Q_target(s) of row b (waves 0-1); threads 128..255: Q_target(s2) of
   // row b - 128 (waves 2-3) -- the two forwards of a row run side by side
   __shared__ __attribute__((aligned(16))) float sw[NET_LDS];
@@ -293,14 +307,15 @@ __global__ void __launch_bounds__(256) k_br_targets(LearnBufs LB, const float* _
   __shared__ uint8_t am[MAX_BATCH];
   __shared__ double part[2];
   __shared__ int lastw[2][3];
+  const TargetJob J = jobs ? jobs[blockIdx.y] : one;
+  if ((int64_t)blockIdx.x >= J.n) return;            // block-uniform
   const int tid = threadIdx.x;
   const int b = tid & (MAX_BATCH - 1);
   const bool s2half = tid >= MAX_BATCH;
-  const int64_t u = u0 + blockIdx.x;
-  const int64_t slot = (int64_t)a * LB.umax + u;
+  const int64_t u = J.u0 + blockIdx.x;
   BrRow rr{};
-  if (b < B) rr = LB.br_rows[slot * B + b];
-  stage_net_lds(sw, tw, tid, blockDim.x);
+  if (b < B) rr = J.rows[u * B + b];
+  stage_net_lds(sw, J.tw, tid, blockDim.x);
   __syncthreads();
   if (b < B) {
     float y[3];
@@ -333,7 +348,7 @@ __global__ void __launch_bounds__(256) k_br_targets(LearnBufs LB, const float* _
     }
   }
   __syncthreads();
-  if (tid == 0) LB.br_expl[slot] = (part[0] + part[1]) / B;
+  if (tid == 0) J.expl[u] = (part[0] + part[1]) / B;
   if (quirks & NFSP_QUIRK_ROW0_TARGET) {
     if (tid < 3) {       // target[0][argmax a_k] = v_k for k = 0..B-1: the last k wins
       const int last = lastw[1][tid] >= 0 ? lastw[1][tid] : lastw[0][tid];
@@ -345,16 +360,16 @@ __global__ void __launch_bounds__(256) k_br_targets(LearnBufs LB, const float* _
   __syncthreads();
   // lr of this update: lr0 / (1 + 0.003 sqrt(iteration)) with iteration = it0 + 2 u
   // (agent/agent.py:249, iteration += 2 per BR update), in the reference's double arithmetic
-  const float lr = (float)(lr0 / (1.0 + 0.003 * sqrt((double)(it0 + 2 * u))));
+  const float lr = (float)(lr0 / (1.0 + 0.003 * sqrt((double)(J.it0 + 2 * u))));
   for (int e = 0; e < E; ++e) {
     uint32_t x = 0;
     float t0 = 0.f, t1 = 0.f, t2 = 0.f;
     if (!s2half && b < B) {
-      const int k = LB.br_perm[(slot * E + e) * B + b];
+      const int k = J.perm[(u * E + e) * B + b];
       x = sb[k];
       t0 = q[k][0]; t1 = q[k][1]; t2 = q[k][2];
     }
-    emit_recs(LB.br_rec + (slot * E + e) * (B / CHAIN_MB), x, t0, t1, t2, lr, B);
+    emit_recs(J.rec + (u * E + e) * (B / CHAIN_MB), x, t0, t1, t2, lr, B);
   }
 }
 
@@ -390,6 +405,28 @@ __global__ void k_finalize(FinalArgs F) {
   }
 }
 
+// engine groups: the AR nets of all replicas <- W0 + sum_r (W_r - W0) / R, and W0 <- that
+// (shards.AvgPolicyAllReduce's exchange, on device, in replica order)
+__global__ void __launch_bounds__(256) k_group_avg_ar(float* const* __restrict__ war /*[R][2]*/,
+                                                      float* __restrict__ w0 /*[2][NP]*/, int R,
+                                                      int broadcast) {
+#pragma clang fp contract(off)
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 2 * nn::NP) return;
+  const int a = i / nn::NP, q = i - a * nn::NP;
+  float nw;
+  if (broadcast) {                      // the first exchange: replica 0's nets everywhere
+    nw = war[a][q];
+  } else {
+    const float base = w0[i];
+    float s = 0.f;
+    for (int r = 0; r < R; ++r) s = s + (war[2 * r + a][q] - base);
+    nw = base + s * (1.0f / (float)R);
+  }
+  w0[i] = nw;
+  for (int r = 0; r < R; ++r) war[2 * r + a][q] = nw;
+}
+
 }  // namespace
 
 #ifdef NFSP_CHAIN_STAMPS
@@ -401,19 +438,31 @@ extern "C" int nfsp_debug_chain_stamps(unsigned long long* out) {
 }
 #endif
 
-extern "C" int nfsp_engine_update(nfsp_engine* e) {
-  NFSP_REQUIRE(e, "null argument");
-  if (!e->pending_update) return NFSP_OK;
-  e->pending_update = false;
-  hipStream_t s = e->ctx->stream;
+namespace {
+
+// ---------------------------------------------------------------------------
+// host side: one learner call = plan (from the rollout's insert counts) + prep launches +
+// chain launches + finalize.  nfsp_engine_update runs them for one engine, the group for
+// R engines with their chains in shared launches.
+// ---------------------------------------------------------------------------
+struct Segment {
+  int64_t u, v;        // BR updates [u, v) of the learner call
+  bool sync;           // ends with a target sync
+};
+
+struct LearnPlan {
+  PrepArgs P;
+  int64_t maxU = 0, maxUbr = 0, maxSL = 0;
+  std::vector<Segment> seg[2];
+  int64_t it0[2];
+  FinalArgs F;
+};
+
+int plan_update(nfsp_engine* e, const EngineDev& h, LearnPlan& L) {
   const nfsp_engine_cfg& cfg = e->cfg;
-  // the trigger plan needs the rollout's insert counts: one small readback
-  EngineDev h;
-  NFSP_HIP(hipMemcpyAsync(&h, e->st, sizeof(h), hipMemcpyDeviceToHost, s));
-  NFSP_HIP(hipStreamSynchronize(s));
-  KTimer kt(e, KT_LEARNER);
   e->learn_tag++;
-  PrepArgs P{};
+  PrepArgs& P = L.P;
+  P = PrepArgs{};
   P.M = e->M;
   P.LB = e->LB;
   P.st = e->st;
@@ -426,7 +475,7 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
   P.tag = e->learn_tag;
   P.lr_ar = cfg.lr_ar;
   P.quirks = cfg.quirks;
-  int64_t maxU = 0, maxUbr = 0, maxSL = 0;
+  L.maxU = L.maxUbr = L.maxSL = 0;
   for (int a = 0; a < 2; ++a) {
     AgentPlan& pl = P.A[a];
     pl.P0 = h.rl_total[a];
@@ -440,83 +489,14 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
     pl.n_sl = h.last_sl[a];
     pl.sl_total0 = h.sl_total[a];
     NFSP_REQUIRE(pl.U <= e->LB.umax, "update plan exceeds the learner buffers");
-    maxU = pl.U > maxU ? pl.U : maxU;
-    maxUbr = pl.U_br > maxUbr ? pl.U_br : maxUbr;
-    maxSL = pl.n_sl > maxSL ? pl.n_sl : maxSL;
+    L.maxU = pl.U > L.maxU ? pl.U : L.maxU;
+    L.maxUbr = pl.U_br > L.maxUbr ? pl.U_br : L.maxUbr;
+    L.maxSL = pl.n_sl > L.maxSL ? pl.n_sl : L.maxSL;
+    e->last_U[a] = pl.U;
+    e->last_Ubr[a] = pl.U_br;
   }
-  {                                    // the BR chain's LDS attribute (AR: chain_ar.hip)
-    static std::atomic<uint64_t> attr{0};
-    const int rc = set_chain_lds(attr, (const void*)k_chain3<1, 0>, (const void*)k_chain3<1, 1>);
-    if (rc != NFSP_OK) return rc;
-  }
-  for (int a = 0; a < 2; ++a) {
-    e->last_U[a] = P.A[a].U;
-    e->last_Ubr[a] = P.A[a].U_br;
-  }
-  // ---- parallel prep on the ctx stream, in the order the chains need it: the BR rows
-  // first (agent 0's BR segments are the learner's critical path), the BR streams fork;
-  // then the AR records, the AR stream forks; the final reservoir last (only the next
-  // rollout reads it, and it must follow k_ar_prep, which reads the reservoir as it was)
-  hipEvent_t fork_br = take_event(e), fork = take_event(e);
-  {
-  KTimer kprep(e, KT_PREP);
-  if (maxUbr > 0) {
-    k_br_prep<<<dim3((unsigned)maxUbr, 2), 128, 0, s>>>(P);
-    NFSP_LAUNCHED("k_br_prep");
-  }
-  if (e->log_loss)                     // NaN = no fit recorded
-    for (int a = 0; a < 2; ++a)
-      NFSP_HIP(hipMemsetAsync(e->LB.br_loss + a * e->LB.umax * cfg.epochs, 0xFF,
-                              sizeof(float) * P.A[a].U_br * cfg.epochs, s));
-  NFSP_HIP(hipEventRecord(fork_br, s));
-  if (maxSL > 0) {
-    k_ar_slots<<<dim3(nfsp_blocks(maxSL, 256), 2), 256, 0, s>>>(P);
-    NFSP_LAUNCHED("k_ar_slots");
-  }
-  if (maxU > 0) {
-    k_ar_prep<<<dim3((unsigned)maxU, 2), 128, 0, s>>>(P);
-    NFSP_LAUNCHED("k_ar_prep");
-  }
-  if (e->log_loss)                     // NaN = no fit recorded (inactive AR update)
-    for (int a = 0; a < 2; ++a)
-      NFSP_HIP(hipMemsetAsync(e->LB.ar_loss + a * e->LB.umax * cfg.epochs, 0xFF,
-                              sizeof(float) * P.A[a].U * cfg.epochs, s));
-  NFSP_HIP(hipEventRecord(fork, s));
-  if (maxSL > 0) {
-    k_res_apply<<<dim3(nfsp_blocks(maxSL, 256), 2), 256, 0, s>>>(P);
-    NFSP_LAUNCHED("k_res_apply");
-  }
-  }
-  // ---- AR chains (both agents, one launch) on their own stream
-  if (maxU > 0) {
-    NFSP_HIP(hipStreamWaitEvent(e->s_ar, fork, 0));
-    ChainArgs C{};
-    C.rec = e->LB.ar_rec;
-    C.loss_out = e->log_loss ? e->LB.ar_loss : nullptr;
-    C.active = e->LB.ar_active;
-    C.umax = e->LB.umax;
-    C.B = cfg.batch;
-    C.E = cfg.epochs;
-    for (int a = 0; a < 2; ++a) {
-      C.agents[a] = a;
-      C.w[a] = e->w + (a * 3 + 0) * nn::NP;
-      C.sync_to[a] = nullptr;
-      C.u0[a] = 0;
-      C.u1[a] = P.A[a].U;
-    }
-    KTimer kc(e, KT_CHAIN_AR, e->s_ar);
-    const int rc = launch_chain_ar(C, 2, C.loss_out != nullptr, e->s_ar);
-    if (rc != NFSP_OK) return rc;
-  }
-  // diagnostic (NFSP_LEARNER_SERIAL=1): BR work waits for the AR chains, to time them alone
-  static const bool serial_ar = getenv("NFSP_LEARNER_SERIAL") && atoi(getenv("NFSP_LEARNER_SERIAL"));
-  hipEvent_t ar_done = fork;
-  if (serial_ar) {
-    ar_done = take_event(e);
-    NFSP_HIP(hipEventRecord(ar_done, e->s_ar));
-  }
-  // ---- BR: per agent, segments between target syncs, each = targets + chain
-  FinalArgs F{};
+  FinalArgs& F = L.F;
+  F = FinalArgs{};
   F.st = e->st;
   F.br_expl = e->LB.br_expl;
   F.umax = e->LB.umax;
@@ -526,52 +506,21 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
     F.n_rl[a] = h.last_rl[a];
     F.n_sl[a] = pl.n_sl;
     F.U_br[a] = pl.U_br;
-    hipStream_t sa = e->s_br[a];
-    NFSP_HIP(hipStreamWaitEvent(sa, serial_ar ? ar_done : fork_br, 0));
     int64_t it = h.iteration[a], tc = h.target_count[a], syncs = h.target_syncs[a];
     double eps = h.epsilon[a];
-    const int64_t it0 = it;
-    float* wbr = e->w + (a * 3 + 1) * nn::NP;
-    float* wtg = e->w + (a * 3 + 2) * nn::NP;
-    int64_t u = 0;
-    while (u < pl.U_br) {
-      // segment [u, v): ends after the first update whose target_count % every == 0
+    L.it0[a] = it;
+    // BR segments between target syncs: [u, v) ends after the first update whose
+    // target_count % every == 0 (agent/agent.py:266-273)
+    L.seg[a].clear();
+    for (int64_t u = 0; u < pl.U_br;) {
       int64_t v = u;
       bool sync = false;
       while (v < pl.U_br) {
-        const bool s_here = (tc + (v - 0)) % cfg.target_every == 0;
+        const bool s_here = (tc + v) % cfg.target_every == 0;
         ++v;
         if (s_here) { sync = true; break; }
       }
-      {
-        KTimer kt2(e, KT_TARGETS, sa);
-        k_br_targets<<<(unsigned)(v - u), 256, 0, sa>>>(e->LB, wtg, a, u, cfg.batch, cfg.epochs,
-                                                         cfg.gamma, cfg.quirks, it0, cfg.lr_br);
-      }
-      NFSP_LAUNCHED("k_br_targets");
-      ChainArgs C{};
-      C.rec = e->LB.br_rec;
-      C.loss_out = e->log_loss ? e->LB.br_loss : nullptr;
-      C.active = nullptr;
-      C.umax = e->LB.umax;
-      C.B = cfg.batch;
-      C.E = cfg.epochs;
-      C.agents[0] = a;
-      C.w[0] = wbr;
-      C.sync_to[0] = sync ? wtg : nullptr;
-      C.u0[0] = u;
-      C.u1[0] = v;
-      {
-        KTimer kc(e, KT_CHAIN_BR, sa);
-        if (cfg.quirks & NFSP_EXT_LINEAR_Q) {
-          const int rc = launch_chain_br_linear(C, C.loss_out != nullptr, sa);
-          if (rc != NFSP_OK) return rc;
-        } else {
-          if (C.loss_out) k_chain3<1, 1><<<1, 256, CHAIN_LDS, sa>>>(C);
-          else k_chain3<1, 0><<<1, 256, CHAIN_LDS, sa>>>(C);
-        }
-      }
-      NFSP_LAUNCHED("k_chain(BR)");
+      L.seg[a].push_back({u, v, sync});
       u = v;
     }
     // schedules (agent/agent.py:245-253, 266-273) in the reference's double arithmetic
@@ -588,6 +537,162 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
     F.temp[a] = 1.0 / (1.0 + 0.02 * sqrt((double)it));
     F.lr[a] = (float)(cfg.lr_br / (1.0 + 0.003 * sqrt((double)it)));
   }
+  return NFSP_OK;
+}
+
+int launch_br_prep(nfsp_engine* e, const LearnPlan& L, hipStream_t s) {
+  if (L.maxUbr > 0) {
+    k_br_prep<<<dim3((unsigned)L.maxUbr, 2), 128, 0, s>>>(L.P);
+    NFSP_LAUNCHED("k_br_prep");
+  }
+  if (e->log_loss)                     // NaN = no fit recorded
+    for (int a = 0; a < 2; ++a)
+      NFSP_HIP(hipMemsetAsync(e->LB.br_loss + a * e->LB.umax * e->cfg.epochs, 0xFF,
+                              sizeof(float) * L.P.A[a].U_br * e->cfg.epochs, s));
+  return NFSP_OK;
+}
+
+int launch_ar_prep(nfsp_engine* e, const LearnPlan& L, hipStream_t s) {
+  if (L.maxSL > 0) {
+    k_ar_slots<<<dim3(nfsp_blocks(L.maxSL, 256), 2), 256, 0, s>>>(L.P);
+    NFSP_LAUNCHED("k_ar_slots");
+  }
+  if (L.maxU > 0) {
+    k_ar_prep<<<dim3((unsigned)L.maxU, 2), 128, 0, s>>>(L.P);
+    NFSP_LAUNCHED("k_ar_prep");
+  }
+  if (e->log_loss)                     // NaN = no fit recorded (inactive AR update)
+    for (int a = 0; a < 2; ++a)
+      NFSP_HIP(hipMemsetAsync(e->LB.ar_loss + a * e->LB.umax * e->cfg.epochs, 0xFF,
+                              sizeof(float) * L.P.A[a].U * e->cfg.epochs, s));
+  return NFSP_OK;
+}
+
+int launch_res_apply(const LearnPlan& L, hipStream_t s) {
+  if (L.maxSL > 0) {
+    k_res_apply<<<dim3(nfsp_blocks(L.maxSL, 256), 2), 256, 0, s>>>(L.P);
+    NFSP_LAUNCHED("k_res_apply");
+  }
+  return NFSP_OK;
+}
+
+int64_t recs_per_update(const nfsp_engine* e) { return (int64_t)e->cfg.epochs * (e->cfg.batch / CHAIN_MB); }
+
+// the AR chain of agent a over the whole learner call
+ChainJob ar_job(const nfsp_engine* e, const LearnPlan& L, int a) {
+  const int64_t um = e->LB.umax;
+  ChainJob j{};
+  j.w = e->w + (a * 3 + 0) * nn::NP;
+  j.sync_to = nullptr;
+  j.rec = e->LB.ar_rec + a * um * recs_per_update(e);
+  j.active = e->LB.ar_active + a * um;
+  j.loss_out = e->log_loss ? e->LB.ar_loss + a * um * e->cfg.epochs : nullptr;
+  j.u0 = 0;
+  j.u1 = L.P.A[a].U;
+  return j;
+}
+
+// BR segment g of agent a: its targets and its chain
+TargetJob br_target_job(const nfsp_engine* e, const LearnPlan& L, int a, const Segment& sg) {
+  const int64_t um = e->LB.umax, B = e->cfg.batch, E = e->cfg.epochs;
+  TargetJob t{};
+  t.rows = e->LB.br_rows + a * um * B;
+  t.perm = e->LB.br_perm + a * um * E * B;
+  t.expl = e->LB.br_expl + a * um;
+  t.rec = e->LB.br_rec + a * um * recs_per_update(e);
+  t.tw = e->w + (a * 3 + 2) * nn::NP;
+  t.u0 = sg.u;
+  t.n = sg.v - sg.u;
+  t.it0 = L.it0[a];
+  return t;
+}
+
+ChainJob br_chain_job(const nfsp_engine* e, int a, const Segment& sg) {
+  const int64_t um = e->LB.umax;
+  ChainJob j{};
+  j.w = e->w + (a * 3 + 1) * nn::NP;
+  j.sync_to = sg.sync ? e->w + (a * 3 + 2) * nn::NP : nullptr;
+  j.rec = e->LB.br_rec + a * um * recs_per_update(e);
+  j.active = nullptr;
+  j.loss_out = e->log_loss ? e->LB.br_loss + a * um * e->cfg.epochs : nullptr;
+  j.u0 = sg.u;
+  j.u1 = sg.v;
+  return j;
+}
+
+int launch_br_chain(const ChainArgs& C, int blocks, unsigned quirks, bool loss_log, hipStream_t s) {
+  if (quirks & NFSP_EXT_LINEAR_Q) return launch_chain_br_linear(C, blocks, loss_log, s);
+  static std::atomic<uint64_t> attr{0};
+  return launch_chain<1>(C, blocks, loss_log, s, attr);
+}
+
+}  // namespace
+
+extern "C" int nfsp_engine_update(nfsp_engine* e) {
+  NFSP_REQUIRE(e, "null argument");
+  NFSP_REQUIRE(e->s_ar, "a replica of an engine group is stepped by nfsp_group_step");
+  if (!e->pending_update) return NFSP_OK;
+  e->pending_update = false;
+  hipStream_t s = e->ctx->stream;
+  const nfsp_engine_cfg& cfg = e->cfg;
+  // the trigger plan needs the rollout's insert counts: one small readback
+  EngineDev h;
+  NFSP_HIP(hipMemcpyAsync(&h, e->st, sizeof(h), hipMemcpyDeviceToHost, s));
+  NFSP_HIP(hipStreamSynchronize(s));
+  KTimer kt(e, KT_LEARNER);
+  LearnPlan L;
+  int rc = plan_update(e, h, L);
+  if (rc != NFSP_OK) return rc;
+  // ---- parallel prep on the ctx stream, in the order the chains need it: the BR rows
+  // first (agent 0's BR segments are the learner's critical path), the BR streams fork;
+  // then the AR records, the AR stream forks; the final reservoir last (only the next
+  // rollout reads it, and it must follow k_ar_prep, which reads the reservoir as it was)
+  hipEvent_t fork_br = take_event(e), fork = take_event(e);
+  {
+    KTimer kprep(e, KT_PREP);
+    if ((rc = launch_br_prep(e, L, s)) != NFSP_OK) return rc;
+    NFSP_HIP(hipEventRecord(fork_br, s));
+    if ((rc = launch_ar_prep(e, L, s)) != NFSP_OK) return rc;
+    NFSP_HIP(hipEventRecord(fork, s));
+    if ((rc = launch_res_apply(L, s)) != NFSP_OK) return rc;
+  }
+  // ---- AR chains (both agents, one launch) on their own stream
+  if (L.maxU > 0) {
+    NFSP_HIP(hipStreamWaitEvent(e->s_ar, fork, 0));
+    ChainArgs C{};
+    C.B = cfg.batch;
+    C.E = cfg.epochs;
+    for (int a = 0; a < 2; ++a) C.job[a] = ar_job(e, L, a);
+    KTimer kc(e, KT_CHAIN_AR, e->s_ar);
+    if ((rc = launch_chain_ar(C, 2, e->log_loss, e->s_ar)) != NFSP_OK) return rc;
+  }
+  // diagnostic (NFSP_LEARNER_SERIAL=1): BR work waits for the AR chains, to time them alone
+  static const bool serial_ar = getenv("NFSP_LEARNER_SERIAL") && atoi(getenv("NFSP_LEARNER_SERIAL"));
+  hipEvent_t ar_done = fork;
+  if (serial_ar) {
+    ar_done = take_event(e);
+    NFSP_HIP(hipEventRecord(ar_done, e->s_ar));
+  }
+  // ---- BR: per agent on its own stream, segments between target syncs = targets + chain
+  for (int a = 0; a < 2; ++a) {
+    hipStream_t sa = e->s_br[a];
+    NFSP_HIP(hipStreamWaitEvent(sa, serial_ar ? ar_done : fork_br, 0));
+    for (const Segment& sg : L.seg[a]) {
+      {
+        KTimer kt2(e, KT_TARGETS, sa);
+        k_br_targets<<<(unsigned)(sg.v - sg.u), 256, 0, sa>>>(nullptr, br_target_job(e, L, a, sg),
+                                                                cfg.batch, cfg.epochs, cfg.gamma,
+                                                                cfg.quirks, cfg.lr_br);
+      }
+      NFSP_LAUNCHED("k_br_targets");
+      ChainArgs C{};
+      C.B = cfg.batch;
+      C.E = cfg.epochs;
+      C.job[0] = br_chain_job(e, a, sg);
+      KTimer kc(e, KT_CHAIN_BR, sa);
+      if ((rc = launch_br_chain(C, 1, cfg.quirks, e->log_loss, sa)) != NFSP_OK) return rc;
+    }
+  }
   // ---- join and publish the schedules
   for (hipStream_t st : {e->s_ar, e->s_br[0], e->s_br[1]}) {
     hipEvent_t j = take_event(e);
@@ -598,7 +703,262 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
   e->pool.push_back(fork);
   e->pool.push_back(fork_br);
   if (ar_done != fork) e->pool.push_back(ar_done);
-  k_finalize<<<1, 64, 0, s>>>(F);
+  k_finalize<<<1, 64, 0, s>>>(L.F);
   NFSP_LAUNCHED("k_finalize");
+  return NFSP_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Engine groups (nfsp_group_*): R replicas stepped together, their chains in shared launches
+// ---------------------------------------------------------------------------
+struct nfsp_group {
+  nfsp_ctx* ctx = nullptr;
+  int R = 0;
+  unsigned flags = 0;
+  std::vector<nfsp_engine*> eng;
+  hipStream_t s_ar = nullptr, s_br = nullptr;
+  // job tables: host (pinned) staging -> device, one copy per learner call
+  char* h_tab = nullptr;
+  char* d_tab = nullptr;
+  size_t tab_cap = 0;
+  float** d_war = nullptr;       // [R][2] AR weight pointers (k_group_avg_ar)
+  float* w0 = nullptr;           // [2][NP] the AR nets after the last exchange
+  bool w0_valid = false;
+  int64_t rounds = 0;            // BR rounds of the last learner call (stats)
+};
+
+extern "C" int nfsp_group_destroy(nfsp_group* g) {
+  if (!g) return NFSP_OK;
+  if (g->ctx) (void)hipStreamSynchronize(g->ctx->stream);
+  for (hipStream_t st : {g->s_ar, g->s_br})
+    if (st) (void)hipStreamSynchronize(st);
+  for (nfsp_engine* e : g->eng) nfsp_engine_destroy(e);
+  if (g->h_tab) (void)hipHostFree(g->h_tab);
+  if (g->d_tab) (void)hipFree(g->d_tab);
+  if (g->d_war) (void)hipFree(g->d_war);
+  if (g->w0) (void)hipFree(g->w0);
+  for (hipStream_t st : {g->s_ar, g->s_br})
+    if (st) (void)hipStreamDestroy(st);
+  delete g;
+  return NFSP_OK;
+}
+
+extern "C" int nfsp_group_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, int replicas, unsigned flags,
+                                 nfsp_group** out) {
+  NFSP_REQUIRE(ctx && cfg && out, "null argument");
+  NFSP_REQUIRE(replicas >= 1 && replicas <= NFSP_GROUP_MAX_REPLICAS, "replicas must be in [1, 64]");
+  NFSP_REQUIRE((flags & ~NFSP_GROUP_AVG_AR) == 0, "unknown group flags");
+  *out = nullptr;
+  nfsp_group* g = new nfsp_group();
+  g->ctx = ctx;
+  g->R = replicas;
+  g->flags = flags;
+  for (int r = 0; r < replicas; ++r) {
+    nfsp_engine_cfg c = *cfg;
+    c.seed = cfg->seed + (uint64_t)r;
+    nfsp_engine* e = nullptr;
+    const int rc = nfsp::eng::engine_create(ctx, &c, false, &e);
+    if (rc != NFSP_OK) {
+      nfsp_group_destroy(g);
+      return rc;
+    }
+    g->eng.push_back(e);
+  }
+  for (hipStream_t* st : {&g->s_ar, &g->s_br}) {
+    const hipError_t sr = hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+    if (sr != hipSuccess) {
+      nfsp_group_destroy(g);
+      return nfsp::hip_fail(sr, "nfsp_group_create: hipStreamCreate");
+    }
+  }
+  std::vector<float*> war(2 * replicas);
+  for (int r = 0; r < replicas; ++r)
+    for (int a = 0; a < 2; ++a) war[2 * r + a] = g->eng[r]->w + (a * 3 + 0) * nn::NP;
+  hipError_t r = hipMalloc((void**)&g->d_war, sizeof(float*) * war.size());
+  if (r == hipSuccess) r = hipMalloc((void**)&g->w0, sizeof(float) * 2 * nn::NP);
+  if (r == hipSuccess) r = hipMemcpy(g->d_war, war.data(), sizeof(float*) * war.size(), hipMemcpyHostToDevice);
+  if (r != hipSuccess) {
+    nfsp_group_destroy(g);
+    return nfsp::hip_fail(r, "nfsp_group_create");
+  }
+  *out = g;
+  return NFSP_OK;
+}
+
+extern "C" int nfsp_group_engine(nfsp_group* g, int r, nfsp_engine** out) {
+  NFSP_REQUIRE(g && out && r >= 0 && r < g->R, "bad argument");
+  *out = g->eng[r];
+  return NFSP_OK;
+}
+
+extern "C" int nfsp_group_average_ar(nfsp_group* g) {
+  NFSP_REQUIRE(g, "null argument");
+  k_group_avg_ar<<<nfsp_blocks(2 * nn::NP, 256), 256, 0, g->ctx->stream>>>(g->d_war, g->w0, g->R,
+                                                                           g->w0_valid ? 0 : 1);
+  NFSP_LAUNCHED("k_group_avg_ar");
+  g->w0_valid = true;
+  return NFSP_OK;
+}
+
+static int group_update(nfsp_group* g) {
+  hipStream_t s = g->ctx->stream;
+  const int R = g->R;
+  nfsp_engine* e0 = g->eng[0];
+  const nfsp_engine_cfg& cfg = e0->cfg;
+  std::vector<EngineDev> h(R);
+  for (int r = 0; r < R; ++r) {
+    NFSP_REQUIRE(g->eng[r]->pending_update, "group replica without a rollout");
+    NFSP_HIP(hipMemcpyAsync(&h[r], g->eng[r]->st, sizeof(EngineDev), hipMemcpyDeviceToHost, s));
+  }
+  NFSP_HIP(hipStreamSynchronize(s));
+  KTimer kt(e0, KT_LEARNER);
+  std::vector<LearnPlan> L(R);
+  int rc;
+  for (int r = 0; r < R; ++r) {
+    g->eng[r]->pending_update = false;
+    if ((rc = plan_update(g->eng[r], h[r], L[r])) != NFSP_OK) return rc;
+  }
+  // ---- job tables: the AR chains (2R workgroups, one launch), then per BR round k the
+  // targets and the chain of every (replica, agent) that has a k-th segment
+  std::vector<ChainJob> ar_jobs;
+  int64_t maxU = 0;
+  for (int r = 0; r < R; ++r)
+    for (int a = 0; a < 2; ++a)
+      if (L[r].P.A[a].U > 0) {
+        ar_jobs.push_back(ar_job(g->eng[r], L[r], a));
+        maxU = L[r].P.A[a].U > maxU ? L[r].P.A[a].U : maxU;
+      }
+  size_t rounds = 0;
+  for (int r = 0; r < R; ++r)
+    for (int a = 0; a < 2; ++a) rounds = L[r].seg[a].size() > rounds ? L[r].seg[a].size() : rounds;
+  std::vector<ChainJob> br_jobs;
+  std::vector<TargetJob> tg_jobs;
+  std::vector<size_t> round_off(rounds + 1, 0);
+  std::vector<int64_t> round_n(rounds, 0);
+  for (size_t k = 0; k < rounds; ++k) {
+    round_off[k] = br_jobs.size();
+    for (int r = 0; r < R; ++r)
+      for (int a = 0; a < 2; ++a)
+        if (k < L[r].seg[a].size()) {
+          const Segment& sg = L[r].seg[a][k];
+          br_jobs.push_back(br_chain_job(g->eng[r], a, sg));
+          tg_jobs.push_back(br_target_job(g->eng[r], L[r], a, sg));
+          round_n[k] = sg.v - sg.u > round_n[k] ? sg.v - sg.u : round_n[k];
+        }
+  }
+  round_off[rounds] = br_jobs.size();
+  g->rounds = (int64_t)rounds;
+  const size_t nb_ar = sizeof(ChainJob) * ar_jobs.size(), nb_br = sizeof(ChainJob) * br_jobs.size();
+  const size_t nb_tg = sizeof(TargetJob) * tg_jobs.size();
+  const size_t need = nb_ar + nb_br + nb_tg;
+  if (need > g->tab_cap) {     // every earlier use of the tables completed (the sync above)
+    if (g->h_tab) NFSP_HIP(hipHostFree(g->h_tab));
+    if (g->d_tab) NFSP_HIP(hipFree(g->d_tab));
+    g->h_tab = nullptr;
+    g->d_tab = nullptr;
+    g->tab_cap = 0;
+    const size_t cap = need * 2;
+    NFSP_HIP(hipHostMalloc((void**)&g->h_tab, cap, hipHostMallocDefault));
+    NFSP_HIP(hipMalloc((void**)&g->d_tab, cap));
+    g->tab_cap = cap;
+  }
+  memcpy(g->h_tab, ar_jobs.data(), nb_ar);
+  memcpy(g->h_tab + nb_ar, br_jobs.data(), nb_br);
+  memcpy(g->h_tab + nb_ar + nb_br, tg_jobs.data(), nb_tg);
+  const ChainJob* d_ar = reinterpret_cast<const ChainJob*>(g->d_tab);
+  const ChainJob* d_br = reinterpret_cast<const ChainJob*>(g->d_tab + nb_ar);
+  const TargetJob* d_tg = reinterpret_cast<const TargetJob*>(g->d_tab + nb_ar + nb_br);
+  hipEvent_t fork_br = take_event(e0), fork = take_event(e0);
+  {
+    KTimer kprep(e0, KT_PREP);
+    if (need > 0) NFSP_HIP(hipMemcpyAsync(g->d_tab, g->h_tab, need, hipMemcpyHostToDevice, s));
+    for (int r = 0; r < R; ++r)
+      if ((rc = launch_br_prep(g->eng[r], L[r], s)) != NFSP_OK) return rc;
+    NFSP_HIP(hipEventRecord(fork_br, s));
+    for (int r = 0; r < R; ++r)
+      if ((rc = launch_ar_prep(g->eng[r], L[r], s)) != NFSP_OK) return rc;
+    NFSP_HIP(hipEventRecord(fork, s));
+    for (int r = 0; r < R; ++r)
+      if ((rc = launch_res_apply(L[r], s)) != NFSP_OK) return rc;
+  }
+  const bool loss_log = e0->log_loss;
+  for (nfsp_engine* e : g->eng)
+    NFSP_REQUIRE(e->log_loss == loss_log, "the loss log must be on in all replicas of a group or none");
+  if (!ar_jobs.empty()) {
+    NFSP_HIP(hipStreamWaitEvent(g->s_ar, fork, 0));
+    ChainArgs C{};
+    C.jobs = d_ar;
+    C.B = cfg.batch;
+    C.E = cfg.epochs;
+    KTimer kc(e0, KT_CHAIN_AR, g->s_ar);
+    if ((rc = launch_chain_ar(C, (int)ar_jobs.size(), loss_log, g->s_ar)) != NFSP_OK) return rc;
+  }
+  NFSP_HIP(hipStreamWaitEvent(g->s_br, fork_br, 0));
+  for (size_t k = 0; k < rounds; ++k) {
+    const int nj = (int)(round_off[k + 1] - round_off[k]);
+    {
+      KTimer kt2(e0, KT_TARGETS, g->s_br);
+      k_br_targets<<<dim3((unsigned)round_n[k], (unsigned)nj), 256, 0, g->s_br>>>(
+          d_tg + round_off[k], TargetJob{}, cfg.batch, cfg.epochs, cfg.gamma, cfg.quirks, cfg.lr_br);
+    }
+    NFSP_LAUNCHED("k_br_targets");
+    ChainArgs C{};
+    C.jobs = d_br + round_off[k];
+    C.B = cfg.batch;
+    C.E = cfg.epochs;
+    KTimer kc(e0, KT_CHAIN_BR, g->s_br);
+    if ((rc = launch_br_chain(C, nj, cfg.quirks, loss_log, g->s_br)) != NFSP_OK) return rc;
+  }
+  for (hipStream_t st : {g->s_ar, g->s_br}) {
+    hipEvent_t j = take_event(e0);
+    NFSP_HIP(hipEventRecord(j, st));
+    NFSP_HIP(hipStreamWaitEvent(s, j, 0));
+    e0->pool.push_back(j);
+  }
+  e0->pool.push_back(fork);
+  e0->pool.push_back(fork_br);
+  for (int r = 0; r < R; ++r) {
+    k_finalize<<<1, 64, 0, s>>>(L[r].F);
+    NFSP_LAUNCHED("k_finalize");
+  }
+  (void)maxU;
+  return NFSP_OK;
+}
+
+extern "C" int nfsp_group_set_timing(nfsp_group* g, int on) {
+  NFSP_REQUIRE(g, "null argument");
+  for (nfsp_engine* e : g->eng) e->timing = on != 0;
+  return NFSP_OK;
+}
+
+// the replicas' rollout / prep marks and the group's shared launches (kept on replica 0)
+extern "C" int nfsp_group_get_timings(nfsp_group* g, double* ms, int64_t* launches) {
+  NFSP_REQUIRE(g && ms && launches, "null argument");
+  for (int k = 0; k < KT_N; ++k) { ms[k] = 0.0; launches[k] = 0; }
+  for (nfsp_engine* e : g->eng) {
+    double m[KT_N];
+    int64_t n[KT_N];
+    const int rc = nfsp_engine_get_timings(e, m, n);
+    if (rc != NFSP_OK) return rc;
+    for (int k = 0; k < KT_N; ++k) { ms[k] += m[k]; launches[k] += n[k]; }
+  }
+  return NFSP_OK;
+}
+
+extern "C" int nfsp_group_step(nfsp_group* g) {
+  NFSP_REQUIRE(g, "null argument");
+  int rc;
+  if ((g->flags & NFSP_GROUP_AVG_AR) && !g->w0_valid)      // common AR nets before the first step
+    if ((rc = nfsp_group_average_ar(g)) != NFSP_OK) return rc;
+  for (nfsp_engine* e : g->eng)
+    if ((rc = nfsp::eng::rollout_launch(e)) != NFSP_OK) return rc;
+  if ((rc = group_update(g)) != NFSP_OK) return rc;
+  if (g->flags & NFSP_GROUP_AVG_AR) return nfsp_group_average_ar(g);
+  return NFSP_OK;
+}
+
+extern "C" int nfsp_group_rounds(nfsp_group* g, int64_t* out) {
+  NFSP_REQUIRE(g && out, "null argument");
+  *out = g->rounds;
   return NFSP_OK;
 }

@@ -38,23 +38,36 @@ def glorot_net(rng: np.random.RandomState, hidden: int = 64) -> np.ndarray:
                            g(hidden, 3).ravel(), np.zeros(3, np.float32)])
 
 
+def make_cfg(L, **cfg) -> native.EngineCfg:
+    c = native.EngineCfg()
+    native.check(L.nfsp_engine_default_cfg(C.byref(c)), "nfsp_engine_default_cfg")
+    for k, v in cfg.items():
+        if not hasattr(c, k):
+            raise KeyError(k)
+        setattr(c, k, v)
+    return c
+
+
 class SelfPlayEngine:
     def __init__(self, ctx: native.Context | None = None, init_seed: int = 0, game: int = native.GAME_LEDUC,
-                 **cfg):
+                 _borrow=None, **cfg):
         self.ctx = ctx if ctx is not None else native.Context(1, game=game)
         L = self.ctx.L
-        c = native.EngineCfg()
-        native.check(L.nfsp_engine_default_cfg(C.byref(c)), "nfsp_engine_default_cfg")
-        for k, v in cfg.items():
-            if not hasattr(c, k):
-                raise KeyError(k)
-            setattr(c, k, v)
+        self.L = L
+        self.dev = torch.device("cuda", torch.cuda.current_device())
+        if _borrow is not None:            # a replica of an EngineGroup: (group, handle, cfg)
+            self._owner, self.h, self.cfg = _borrow
+            self._init_weights(init_seed)
+            return
+        self._owner = None
+        c = make_cfg(L, **cfg)
         self.cfg = c
         h = native.P()
         native.check(L.nfsp_engine_create(self.ctx.h, C.byref(c), C.byref(h)), "nfsp_engine_create")
         self.h = h
-        self.L = L
-        self.dev = torch.device("cuda", torch.cuda.current_device())
+        self._init_weights(init_seed)
+
+    def _init_weights(self, init_seed):
         # initial weights in the reference's construction order: per agent AR, BR, target
         # (the target is drawn, then overwritten with BR: agent/agent.py:67-72)
         rng = np.random.RandomState(init_seed)
@@ -178,8 +191,85 @@ class SelfPlayEngine:
         return exploitability(self.ctx, self._wptr(0, NET_AR), self._wptr(1, NET_AR), mode)
 
     def close(self):
-        if getattr(self, "h", None):
+        if getattr(self, "h", None) and getattr(self, "_owner", None) is None:
             self.L.nfsp_engine_destroy(self.h)
+        self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class EngineGroup:
+    """R replicas of the engine stepped together (``nfsp_group_*``, include/nfsp.h): each an
+    independent main.train over ``n_lanes`` lanes with its own memories and nets (seed + r,
+    initial nets from ``init_seed + r`` -- replica r is bit-identical to
+    ``SelfPlayEngine(seed=seed + r, init_seed=init_seed + r)``), their SGD chains in shared
+    launches.  ``avg_ar``: the AR nets are averaged over the replicas after every step (C4's
+    exchange on device, shards.AvgPolicyAllReduce)."""
+
+    def __init__(self, replicas: int, ctx: native.Context | None = None, init_seed: int = 0,
+                 game: int = native.GAME_LEDUC, avg_ar: bool = False, **cfg):
+        self.ctx = ctx if ctx is not None else native.Context(1, game=game)
+        self.L = self.ctx.L
+        self.cfg = make_cfg(self.L, **cfg)
+        h = native.P()
+        native.check(self.L.nfsp_group_create(self.ctx.h, C.byref(self.cfg), int(replicas),
+                                              native.GROUP_AVG_AR if avg_ar else 0, C.byref(h)),
+                     "nfsp_group_create")
+        self.h = h
+        self.R = int(replicas)
+        self.replicas = []
+        for r in range(self.R):
+            e = native.P()
+            native.check(self.L.nfsp_group_engine(self.h, r, C.byref(e)), "nfsp_group_engine")
+            c = native.EngineCfg.from_buffer_copy(self.cfg)
+            c.seed = self.cfg.seed + r
+            self.replicas.append(SelfPlayEngine(self.ctx, init_seed=init_seed + r, _borrow=(self, e, c)))
+
+    def step(self):
+        native.check(self.L.nfsp_group_step(self.h), "nfsp_group_step")
+
+    def average_ar(self):
+        native.check(self.L.nfsp_group_average_ar(self.h), "nfsp_group_average_ar")
+
+    def rounds(self) -> int:
+        n = native.I64()
+        native.check(self.L.nfsp_group_rounds(self.h, C.byref(n)), "nfsp_group_rounds")
+        return n.value
+
+    def stats(self) -> dict:
+        """Per-replica stats summed (counters) and listed (``replicas``)."""
+        per = [e.stats() for e in self.replicas]
+        out = {"replicas": per}
+        for k in ("hands", "rollouts"):
+            out[k] = sum(p[k] for p in per)
+        for k in ("rl_total", "sl_total", "br_updates", "ar_updates", "last_rl", "last_sl"):
+            out[k] = [sum(p[k][a] for p in per) for a in (0, 1)]
+        out["exploitability"] = [float(np.mean([p["exploitability"][a] for p in per])) for a in (0, 1)]
+        return out
+
+    KERNELS = SelfPlayEngine.KERNELS
+
+    def set_timing(self, on=True):
+        native.check(self.L.nfsp_group_set_timing(self.h, int(bool(on))), "set_timing")
+
+    def timings(self) -> dict:
+        ms = (native.F64 * 8)()
+        n = (native.I64 * 8)()
+        native.check(self.L.nfsp_group_get_timings(self.h, ms, n), "get_timings")
+        return {k: (ms[i], n[i]) for i, k in enumerate(self.KERNELS)}
+
+    def exploitability(self, mode: int = 0, replica: int = 0) -> dict:
+        return self.replicas[replica].exploitability(mode)
+
+    def close(self):
+        if getattr(self, "h", None):
+            for e in self.replicas:
+                e.h = None
+            self.L.nfsp_group_destroy(self.h)
             self.h = None
 
     def __del__(self):

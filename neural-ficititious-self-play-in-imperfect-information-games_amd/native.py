@@ -103,7 +103,17 @@ SIGNATURES = {
     "nfsp_engine_losses": (I32, [P, P]),
     "nfsp_engine_set_timing": (I32, [P, I32]),
     "nfsp_engine_get_timings": (I32, [P, C.POINTER(F64), C.POINTER(I64)]),
+    "nfsp_group_create": (I32, [P, C.POINTER(EngineCfg), I32, U32, C.POINTER(P)]),
+    "nfsp_group_destroy": (I32, [P]),
+    "nfsp_group_engine": (I32, [P, I32, C.POINTER(P)]),
+    "nfsp_group_step": (I32, [P]),
+    "nfsp_group_average_ar": (I32, [P]),
+    "nfsp_group_set_timing": (I32, [P, I32]),
+    "nfsp_group_get_timings": (I32, [P, C.POINTER(F64), C.POINTER(I64)]),
+    "nfsp_group_rounds": (I32, [P, C.POINTER(I64)]),
 }
+GROUP_AVG_AR = 1
+GROUP_MAX_REPLICAS = 64
 
 _LIB = None
 

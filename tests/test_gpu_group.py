@@ -1,0 +1,117 @@
+"""Engine groups (nfsp_group_*): R replicas stepped together, their SGD chains in shared
+launches (one AR launch of 2R workgroups, BR rounds of every (replica, agent)'s k-th
+target-sync segment).
+
+Bar: replica r of a group is BIT-IDENTICAL to a standalone engine with seed + r and
+init_seed + r stepped as often -- every net, the memories, the counters and schedules.
+The standalone engine is itself pinned to the oracle (test_gpu_engine / test_gpu_learner),
+so this carries that parity over to the grouped launches.  With the AR exchange on, the AR
+nets equal shards.AvgPolicyAllReduce's W0 + sum_r (W_r - W0) / R, recomputed here in numpy
+f32 in replica order from standalone engines stepped from the same common nets."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+# small memories (M_RL wraps, M_SL replaces) and a short target-sync period, so one step has
+# several BR rounds whose segments differ between replicas and agents
+SMALL = dict(n_lanes=2048, rl_capacity=3000, sl_capacity=2000, target_every=7)
+
+
+def nets(eng):
+    return [eng.get_weights(a, n) for a in (0, 1) for n in (0, 1, 2)]
+
+
+def mem(eng, a):
+    m = eng.memories(a)
+    torch.cuda.synchronize()
+    return {k: v.cpu().numpy() for k, v in m.items() if isinstance(v, torch.Tensor)}
+
+
+STAT_KEYS = ("hands", "rl_total", "sl_total", "rl_size", "sl_size", "br_updates", "ar_updates",
+             "iteration", "target_syncs", "actions", "reward", "epsilon", "temp", "lr_br",
+             "exploitability")
+
+
+@pytest.mark.parametrize("quirks,R", [(None, 3), (120, 2)])
+def test_group_replicas_match_standalone_engines(pkg, quirks, R):
+    kw = dict(SMALL)
+    if quirks is not None:
+        kw["quirks"] = quirks
+    g = pkg.engine.EngineGroup(R, seed=777, init_seed=5, **kw)
+    solo = [pkg.engine.SelfPlayEngine(seed=777 + r, init_seed=5 + r, **kw) for r in range(R)]
+    for step in range(3):
+        g.step()
+        for e in solo:
+            e.step()
+        torch.cuda.synchronize()
+        assert g.rounds() >= 2
+        for r in range(R):
+            a_st, b_st = g.replicas[r].stats(), solo[r].stats()
+            for k in STAT_KEYS:
+                assert a_st[k] == b_st[k], (step, r, k, a_st[k], b_st[k])
+            for x, y in zip(nets(g.replicas[r]), nets(solo[r])):
+                assert np.array_equal(x, y), (step, r)
+    for r in range(R):
+        for a in (0, 1):
+            ma, mb = mem(g.replicas[r], a), mem(solo[r], a)
+            for k in ma:
+                assert np.array_equal(ma[k], mb[k]), (r, a, k)
+    # replicas differ from each other (own seeds)
+    assert not np.array_equal(nets(g.replicas[0])[0], nets(g.replicas[1])[0])
+
+
+def test_group_loss_log_matches_standalone(pkg):
+    g = pkg.engine.EngineGroup(2, seed=31, init_seed=2, **SMALL)
+    solo = [pkg.engine.SelfPlayEngine(seed=31 + r, init_seed=2 + r, **SMALL) for r in range(2)]
+    for e in g.replicas + solo:
+        e.set_loss_log(True)
+    for _ in range(2):
+        g.step()
+        for e in solo:
+            e.step()
+    for r in range(2):
+        la, lb = g.replicas[r].losses(), solo[r].losses()
+        for k in la:
+            assert (np.isnan(la[k]) and np.isnan(lb[k])) or la[k] == lb[k], (r, k)
+
+
+def test_group_ar_exchange(pkg):
+    """avg_ar: replica 0's AR nets go everywhere first; after each step every replica holds
+    W0 + sum_r (W_r - W0) / R (f32, replica order) of the replicas' own SGD results."""
+    R = 3
+    g = pkg.engine.EngineGroup(R, seed=99, init_seed=0, avg_ar=True, **SMALL)
+    solo = [pkg.engine.SelfPlayEngine(seed=99 + r, init_seed=r, **SMALL) for r in range(R)]
+    w0 = [solo[0].get_weights(a, 0) for a in (0, 1)]
+    for e in solo:
+        for a in (0, 1):
+            e.set_weights(a, 0, w0[a])
+    for step in range(2):
+        g.step()
+        for e in solo:
+            e.step()
+        torch.cuda.synchronize()
+        for a in (0, 1):
+            base = w0[a].astype(np.float32)
+            s = np.zeros_like(base)
+            for e in solo:
+                s = (s + (e.get_weights(a, 0) - base)).astype(np.float32)
+            exp = (base + s * np.float32(1.0 / R)).astype(np.float32)
+            for r in range(R):
+                assert np.array_equal(g.replicas[r].get_weights(a, 0), exp), (step, a, r)
+            w0[a] = exp
+            for e in solo:                          # the standalone side's own exchange
+                e.set_weights(a, 0, exp)
+        # BR nets stay per replica, and equal the standalone engines' (same AR nets acted)
+        for r in range(R):
+            for a in (0, 1):
+                assert np.array_equal(g.replicas[r].get_weights(a, 1), solo[r].get_weights(a, 1))
+
+
+def test_group_replica_refuses_its_own_update(pkg):
+    g = pkg.engine.EngineGroup(2, **SMALL)
+    with pytest.raises(pkg.native.NativeError):
+        g.replicas[0].step()
+    g.step()                                       # the group still steps
+    assert g.stats()["hands"] == 2 * SMALL["n_lanes"]
