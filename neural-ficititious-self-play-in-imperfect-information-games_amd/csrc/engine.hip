@@ -45,7 +45,14 @@ struct RolloutArgs {
   Staging S;
 };
 
-__global__ void __launch_bounds__(256) k_rollout(RolloutArgs A) {
+// One replica's rollout / commit arguments in an engine group's device table.
+struct GroupRollout {
+  RolloutArgs A;
+  Memories M;
+  int nblk;
+};
+
+__device__ __forceinline__ void rollout_body(const RolloutArgs& A, int bx) {
   __shared__ __attribute__((aligned(16))) float sw[4 * NET_LDS];
   __shared__ unsigned s_act[2][3];
   __shared__ int s_rew[2];
@@ -65,7 +72,7 @@ __global__ void __launch_bounds__(256) k_rollout(RolloutArgs A) {
   if (tid < 2) s_rew[tid] = 0;
   __syncthreads();
 
-  const int L = blockIdx.x * blockDim.x + tid;
+  const int L = bx * blockDim.x + tid;
   if (L < A.N) {
     const int N = A.N;
     const double eps0 = A.st->epsilon[0], eps1 = A.st->epsilon[1];
@@ -204,6 +211,17 @@ __global__ void __launch_bounds__(256) k_rollout(RolloutArgs A) {
                                        (unsigned long long)(long long)s_rew[tid]);
 }
 
+__global__ void __launch_bounds__(256) k_rollout(RolloutArgs A) { rollout_body(A, blockIdx.x); }
+
+// engine groups: blockIdx.y = replica (the rollout index is the same for every replica)
+__global__ void __launch_bounds__(256) k_rollout_g(const GroupRollout* __restrict__ tab, uint32_t g_lo,
+                                                   uint32_t g_hi) {
+  RolloutArgs A = tab[blockIdx.y].A;
+  A.g_lo = g_lo;
+  A.g_hi = g_hi;
+  rollout_body(A, blockIdx.x);
+}
+
 // ---------------------------------------------------------------------------
 // scan of the 4 per-lane counts (canonical insert order)
 // ---------------------------------------------------------------------------
@@ -212,12 +230,12 @@ __device__ inline unsigned long long unpack_counts(uint32_t c) {
          ((unsigned long long)((c >> 8) & 15u) << 32) | ((unsigned long long)((c >> 12) & 15u) << 48);
 }
 
-__global__ void __launch_bounds__(256) k_scan1(const uint32_t* __restrict__ counts, int N,
-                                               unsigned long long* __restrict__ local,
-                                               uint4* __restrict__ block_sum) {
+__device__ __forceinline__ void scan1_body(const uint32_t* __restrict__ counts, int N,
+                                           unsigned long long* __restrict__ local,
+                                           uint4* __restrict__ block_sum, int bx) {
   __shared__ unsigned long long wsum[4];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int L = blockIdx.x * 256 + tid;
+  const int L = bx * 256 + tid;
   const unsigned long long v = L < N ? unpack_counts(counts[L]) : 0ull;
   // inclusive wave scan (fields never carry: block totals <= 256 * 4)
   unsigned long long x = v;
@@ -233,13 +251,24 @@ __global__ void __launch_bounds__(256) k_scan1(const uint32_t* __restrict__ coun
   if (L < N) local[L] = pre + x - v;
   if (tid == 255) {
     const unsigned long long tot = pre + x;
-    block_sum[blockIdx.x] = make_uint4((uint32_t)(tot & 0xFFFF), (uint32_t)((tot >> 16) & 0xFFFF),
-                                       (uint32_t)((tot >> 32) & 0xFFFF), (uint32_t)(tot >> 48));
+    block_sum[bx] = make_uint4((uint32_t)(tot & 0xFFFF), (uint32_t)((tot >> 16) & 0xFFFF),
+                               (uint32_t)((tot >> 32) & 0xFFFF), (uint32_t)(tot >> 48));
   }
 }
 
-__global__ void __launch_bounds__(1024) k_scan2(const uint4* __restrict__ block_sum, int nblk,
-                                                uint4* __restrict__ block_base, EngineDev* st) {
+__global__ void __launch_bounds__(256) k_scan1(const uint32_t* __restrict__ counts, int N,
+                                               unsigned long long* __restrict__ local,
+                                               uint4* __restrict__ block_sum) {
+  scan1_body(counts, N, local, block_sum, blockIdx.x);
+}
+
+__global__ void __launch_bounds__(256) k_scan1_g(const GroupRollout* __restrict__ tab) {
+  const RolloutArgs& A = tab[blockIdx.y].A;
+  scan1_body(A.S.counts, A.N, A.S.local, A.S.block_sum, blockIdx.x);
+}
+
+__device__ __forceinline__ void scan2_body(const uint4* __restrict__ block_sum, int nblk,
+                                           uint4* __restrict__ block_base, EngineDev* st) {
   __shared__ uint4 part[1024];
   __shared__ uint4 carry;
   const int tid = threadIdx.x;
@@ -278,12 +307,22 @@ __global__ void __launch_bounds__(1024) k_scan2(const uint4* __restrict__ block_
   }
 }
 
+__global__ void __launch_bounds__(1024) k_scan2(const uint4* __restrict__ block_sum, int nblk,
+                                                uint4* __restrict__ block_base, EngineDev* st) {
+  scan2_body(block_sum, nblk, block_base, st);
+}
+
+__global__ void __launch_bounds__(1024) k_scan2_g(const GroupRollout* __restrict__ tab) {   // block = replica
+  const GroupRollout& T = tab[blockIdx.x];
+  scan2_body(T.A.S.block_sum, T.nblk, T.A.S.block_base, T.A.st);
+}
+
 // ---------------------------------------------------------------------------
 // k_commit: staging -> M_RL logs (fp32 rows) and the pending SL lists
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_commit(int N, unsigned quirks, Staging S, Memories M,
-                                                const EngineDev* __restrict__ st) {
-  const int L = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void commit_body(int N, unsigned quirks, const Staging& S, const Memories& M,
+                                            const EngineDev* __restrict__ st, int bx) {
+  const int L = bx * blockDim.x + threadIdx.x;
   if (L >= N) return;
   const uint32_t cnt = S.counts[L];
   const unsigned long long loc = S.local[L];
@@ -324,6 +363,16 @@ __global__ void __launch_bounds__(256) k_commit(int N, unsigned quirks, Staging 
   }
 }
 
+__global__ void __launch_bounds__(256) k_commit(int N, unsigned quirks, Staging S, Memories M,
+                                                const EngineDev* __restrict__ st) {
+  commit_body(N, quirks, S, M, st, blockIdx.x);
+}
+
+__global__ void __launch_bounds__(256) k_commit_g(const GroupRollout* __restrict__ tab) {
+  const GroupRollout& T = tab[blockIdx.y];
+  commit_body(T.A.N, T.A.quirks, T.A.S, T.M, T.A.st, blockIdx.x);
+}
+
 // the reference's fp32 tuple layout (utils/replay_buffer.py:53-57) of agent a's memories
 __global__ void __launch_bounds__(256) k_export_mem(Memories M, int a) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -355,6 +404,15 @@ __global__ void __launch_bounds__(256) k_export_mem(Memories M, int a) {
 __global__ void k_finish_rollout(EngineDev* st, int64_t N) {
   if (threadIdx.x == 0) {
     st->hands += N;
+    st->rollouts += 1;
+  }
+}
+
+__global__ void k_finish_rollout_g(const GroupRollout* __restrict__ tab, int R) {
+  const int r = threadIdx.x;
+  if (r < R) {
+    EngineDev* st = tab[r].A.st;
+    st->hands += tab[r].A.N;
     st->rollouts += 1;
   }
 }
@@ -542,9 +600,7 @@ extern "C" int nfsp_engine_weights(nfsp_engine* e, int agent, int net, float** d
 
 namespace nfsp {
 namespace eng {
-int rollout_launch(nfsp_engine* e) {
-  NFSP_REQUIRE(!e->pending_update, "nfsp_engine_update must consume the previous rollout first");
-  hipStream_t s = e->ctx->stream;
+static RolloutArgs rollout_args(const nfsp_engine* e) {
   RolloutArgs A;
   A.N = e->N;
   A.k0 = (uint32_t)e->cfg.seed;
@@ -557,6 +613,13 @@ int rollout_launch(nfsp_engine* e) {
   A.w = e->w;
   A.st = e->st;
   A.S = e->S;
+  return A;
+}
+
+int rollout_launch(nfsp_engine* e) {
+  NFSP_REQUIRE(!e->pending_update, "nfsp_engine_update must consume the previous rollout first");
+  hipStream_t s = e->ctx->stream;
+  const RolloutArgs A = rollout_args(e);
   {
     KTimer kt(e, KT_ROLLOUT);
     k_rollout<<<e->nblk, 256, 0, s>>>(A);
@@ -577,6 +640,53 @@ int rollout_launch(nfsp_engine* e) {
   NFSP_LAUNCHED("k_finish_rollout");
   e->rollouts++;
   e->pending_update = true;
+  return NFSP_OK;
+}
+
+int group_rollout_table(nfsp_engine* const* eng, int R, void** d_tab) {
+  std::vector<GroupRollout> h(R);
+  for (int r = 0; r < R; ++r) {
+    NFSP_REQUIRE(eng[r]->N == eng[0]->N, "group replicas differ in n_lanes");
+    h[r].A = rollout_args(eng[r]);
+    h[r].M = eng[r]->M;
+    h[r].nblk = eng[r]->nblk;
+  }
+  NFSP_HIP(hipMalloc(d_tab, sizeof(GroupRollout) * R));
+  NFSP_HIP(hipMemcpy(*d_tab, h.data(), sizeof(GroupRollout) * R, hipMemcpyHostToDevice));
+  return NFSP_OK;
+}
+
+// every replica's rollout in one launch per kernel (blockIdx.y = replica); the marks are
+// kept on replica 0
+int group_rollout_launch(nfsp_engine* const* eng, int R, const void* d_tab) {
+  nfsp_engine* e0 = eng[0];
+  for (int r = 0; r < R; ++r)
+    NFSP_REQUIRE(!eng[r]->pending_update && eng[r]->rollouts == e0->rollouts,
+                 "group replicas out of step");
+  hipStream_t s = e0->ctx->stream;
+  const GroupRollout* tab = static_cast<const GroupRollout*>(d_tab);
+  {
+    KTimer kt(e0, KT_ROLLOUT);
+    k_rollout_g<<<dim3(e0->nblk, R), 256, 0, s>>>(tab, (uint32_t)e0->rollouts, (uint32_t)(e0->rollouts >> 32));
+  }
+  NFSP_LAUNCHED("k_rollout_g");
+  {
+    KTimer kt(e0, KT_SCAN);
+    k_scan1_g<<<dim3(e0->nblk, R), 256, 0, s>>>(tab);
+    k_scan2_g<<<R, 1024, 0, s>>>(tab);
+  }
+  NFSP_LAUNCHED("k_scan_g");
+  {
+    KTimer kt(e0, KT_COMMIT);
+    k_commit_g<<<dim3(e0->nblk, R), 256, 0, s>>>(tab);
+  }
+  NFSP_LAUNCHED("k_commit_g");
+  k_finish_rollout_g<<<1, 64, 0, s>>>(tab, R);
+  NFSP_LAUNCHED("k_finish_rollout_g");
+  for (int r = 0; r < R; ++r) {
+    eng[r]->rollouts++;
+    eng[r]->pending_update = true;
+  }
   return NFSP_OK;
 }
 }  // namespace eng

@@ -230,7 +230,11 @@ namespace eng {
 
 hipEvent_t take_event(nfsp_engine* e);
 int engine_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, bool own_streams, nfsp_engine** out);
-int rollout_launch(nfsp_engine* e);   // nfsp_rollout's launches (also the group's, per replica)
+int rollout_launch(nfsp_engine* e);   // nfsp_rollout's launches
+// engine groups: the replicas' rollout arguments as a device table (static), and every
+// replica's rollout through it in one launch per kernel
+int group_rollout_table(nfsp_engine* const* eng, int R, void** d_tab);
+int group_rollout_launch(nfsp_engine* const* eng, int R, const void* d_tab);
 
 // RAII bracket: records start/stop events around launches on `stream` when timing is on
 struct KTimer {

@@ -57,7 +57,9 @@ struct PrepArgs {
 // ---------------------------------------------------------------------------
 // BR prep: rows of update u of agent a (agent/agent.py:217 sample_batch)
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(128) k_br_prep(PrepArgs P) {
+template <int TABLE>   // TABLE: engine groups, blockIdx.z = replica of `tab`
+__global__ void __launch_bounds__(128) k_br_prep(PrepArgs P0, const PrepArgs* __restrict__ tab) {
+  const PrepArgs& P = TABLE ? tab[blockIdx.z] : P0;
   __shared__ int64_t cand[MAX_BATCH];
   __shared__ uint32_t key[MAX_BATCH];
   const int a = blockIdx.y;
@@ -95,7 +97,9 @@ __global__ void __launch_bounds__(128) k_br_prep(PrepArgs P) {
 // ---------------------------------------------------------------------------
 // reservoir slots + per-slot insert lists (utils/ReservoirBuffer.py:18-28)
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_ar_slots(PrepArgs P) {
+template <int TABLE>   // TABLE: engine groups, blockIdx.z = replica of `tab`
+__global__ void __launch_bounds__(256) k_ar_slots(PrepArgs P0, const PrepArgs* __restrict__ tab) {
+  const PrepArgs& P = TABLE ? tab[blockIdx.z] : P0;
   const int a = blockIdx.y;
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const AgentPlan& pl = P.A[a];
@@ -184,7 +188,9 @@ __device__ inline int64_t latest_insert(const LearnBufs& LB, const Memories& M, 
 // ---------------------------------------------------------------------------
 // AR prep (agent/agent.py:259-261): M_SL as it was at the trigger
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(128) k_ar_prep(PrepArgs P) {
+template <int TABLE>   // TABLE: engine groups, blockIdx.z = replica of `tab`
+__global__ void __launch_bounds__(128) k_ar_prep(PrepArgs P0, const PrepArgs* __restrict__ tab) {
+  const PrepArgs& P = TABLE ? tab[blockIdx.z] : P0;
   __shared__ int64_t cand[MAX_BATCH];
   __shared__ uint32_t key[MAX_BATCH];
   __shared__ uint32_t rx[MAX_BATCH];
@@ -263,7 +269,9 @@ __global__ void __launch_bounds__(128) k_ar_prep(PrepArgs P) {
   if (last && b < P.B) P.M.dbg_rows[dbg * P.B + b] = cand[b];
 }
 
-__global__ void __launch_bounds__(256) k_res_apply(PrepArgs P) {
+template <int TABLE>   // TABLE: engine groups, blockIdx.z = replica of `tab`
+__global__ void __launch_bounds__(256) k_res_apply(PrepArgs P0, const PrepArgs* __restrict__ tab) {
+  const PrepArgs& P = TABLE ? tab[blockIdx.z] : P0;
   const int a = blockIdx.y;
   const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= P.A[a].n_sl) return;
@@ -385,7 +393,9 @@ struct FinalArgs {
   int64_t sl_cap;
 };
 
-__global__ void k_finalize(FinalArgs F) {
+template <int TABLE>   // TABLE: engine groups, block = replica of `tab`
+__global__ void k_finalize(FinalArgs F0, const FinalArgs* __restrict__ tab) {
+  const FinalArgs& F = TABLE ? tab[blockIdx.x] : F0;
   if (threadIdx.x != 0) return;
   for (int a = 0; a < 2; ++a) {
     EngineDev* st = F.st;
@@ -542,7 +552,7 @@ int plan_update(nfsp_engine* e, const EngineDev& h, LearnPlan& L) {
 
 int launch_br_prep(nfsp_engine* e, const LearnPlan& L, hipStream_t s) {
   if (L.maxUbr > 0) {
-    k_br_prep<<<dim3((unsigned)L.maxUbr, 2), 128, 0, s>>>(L.P);
+    k_br_prep<0><<<dim3((unsigned)L.maxUbr, 2), 128, 0, s>>>(L.P, nullptr);
     NFSP_LAUNCHED("k_br_prep");
   }
   if (e->log_loss)                     // NaN = no fit recorded
@@ -554,11 +564,11 @@ int launch_br_prep(nfsp_engine* e, const LearnPlan& L, hipStream_t s) {
 
 int launch_ar_prep(nfsp_engine* e, const LearnPlan& L, hipStream_t s) {
   if (L.maxSL > 0) {
-    k_ar_slots<<<dim3(nfsp_blocks(L.maxSL, 256), 2), 256, 0, s>>>(L.P);
+    k_ar_slots<0><<<dim3(nfsp_blocks(L.maxSL, 256), 2), 256, 0, s>>>(L.P, nullptr);
     NFSP_LAUNCHED("k_ar_slots");
   }
   if (L.maxU > 0) {
-    k_ar_prep<<<dim3((unsigned)L.maxU, 2), 128, 0, s>>>(L.P);
+    k_ar_prep<0><<<dim3((unsigned)L.maxU, 2), 128, 0, s>>>(L.P, nullptr);
     NFSP_LAUNCHED("k_ar_prep");
   }
   if (e->log_loss)                     // NaN = no fit recorded (inactive AR update)
@@ -570,7 +580,7 @@ int launch_ar_prep(nfsp_engine* e, const LearnPlan& L, hipStream_t s) {
 
 int launch_res_apply(const LearnPlan& L, hipStream_t s) {
   if (L.maxSL > 0) {
-    k_res_apply<<<dim3(nfsp_blocks(L.maxSL, 256), 2), 256, 0, s>>>(L.P);
+    k_res_apply<0><<<dim3(nfsp_blocks(L.maxSL, 256), 2), 256, 0, s>>>(L.P, nullptr);
     NFSP_LAUNCHED("k_res_apply");
   }
   return NFSP_OK;
@@ -703,7 +713,7 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
   e->pool.push_back(fork);
   e->pool.push_back(fork_br);
   if (ar_done != fork) e->pool.push_back(ar_done);
-  k_finalize<<<1, 64, 0, s>>>(L.F);
+  k_finalize<0><<<1, 64, 0, s>>>(L.F, nullptr);
   NFSP_LAUNCHED("k_finalize");
   return NFSP_OK;
 }
@@ -717,15 +727,31 @@ struct nfsp_group {
   unsigned flags = 0;
   std::vector<nfsp_engine*> eng;
   hipStream_t s_ar = nullptr, s_br = nullptr;
-  // job tables: host (pinned) staging -> device, one copy per learner call
+  void* d_roll = nullptr;        // the replicas' rollout arguments (static device table)
+  // per learner call: job / prep / final tables, host (pinned) staging -> device, one copy
   char* h_tab = nullptr;
   char* d_tab = nullptr;
   size_t tab_cap = 0;
+  // the replicas' EngineDev, gathered on device and read back in one copy
+  EngineDev** d_stp = nullptr;   // [R] -> each replica's state
+  EngineDev* d_st = nullptr;     // [R]
+  EngineDev* h_st = nullptr;     // [R] pinned
   float** d_war = nullptr;       // [R][2] AR weight pointers (k_group_avg_ar)
   float* w0 = nullptr;           // [2][NP] the AR nets after the last exchange
   bool w0_valid = false;
   int64_t rounds = 0;            // BR rounds of the last learner call (stats)
 };
+
+namespace {
+__global__ void k_gather_st(EngineDev* const* __restrict__ src, EngineDev* __restrict__ dst, int R) {
+  constexpr int W = (int)(sizeof(EngineDev) / 8);
+  static_assert(sizeof(EngineDev) % 8 == 0, "EngineDev words");
+  for (int i = threadIdx.x; i < R * W; i += blockDim.x) {
+    const int r = i / W, k = i - r * W;
+    reinterpret_cast<uint64_t*>(dst + r)[k] = reinterpret_cast<const uint64_t*>(src[r])[k];
+  }
+}
+}  // namespace
 
 extern "C" int nfsp_group_destroy(nfsp_group* g) {
   if (!g) return NFSP_OK;
@@ -734,9 +760,9 @@ extern "C" int nfsp_group_destroy(nfsp_group* g) {
     if (st) (void)hipStreamSynchronize(st);
   for (nfsp_engine* e : g->eng) nfsp_engine_destroy(e);
   if (g->h_tab) (void)hipHostFree(g->h_tab);
-  if (g->d_tab) (void)hipFree(g->d_tab);
-  if (g->d_war) (void)hipFree(g->d_war);
-  if (g->w0) (void)hipFree(g->w0);
+  if (g->h_st) (void)hipHostFree(g->h_st);
+  for (void* p : {(void*)g->d_tab, (void*)g->d_war, (void*)g->w0, g->d_roll, (void*)g->d_stp, (void*)g->d_st})
+    if (p) (void)hipFree(p);
   for (hipStream_t st : {g->s_ar, g->s_br})
     if (st) (void)hipStreamDestroy(st);
   delete g;
@@ -771,12 +797,24 @@ extern "C" int nfsp_group_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, int 
       return nfsp::hip_fail(sr, "nfsp_group_create: hipStreamCreate");
     }
   }
+  int rc = nfsp::eng::group_rollout_table(g->eng.data(), replicas, &g->d_roll);
+  if (rc != NFSP_OK) {
+    nfsp_group_destroy(g);
+    return rc;
+  }
   std::vector<float*> war(2 * replicas);
-  for (int r = 0; r < replicas; ++r)
+  std::vector<EngineDev*> stp(replicas);
+  for (int r = 0; r < replicas; ++r) {
     for (int a = 0; a < 2; ++a) war[2 * r + a] = g->eng[r]->w + (a * 3 + 0) * nn::NP;
+    stp[r] = g->eng[r]->st;
+  }
   hipError_t r = hipMalloc((void**)&g->d_war, sizeof(float*) * war.size());
   if (r == hipSuccess) r = hipMalloc((void**)&g->w0, sizeof(float) * 2 * nn::NP);
   if (r == hipSuccess) r = hipMemcpy(g->d_war, war.data(), sizeof(float*) * war.size(), hipMemcpyHostToDevice);
+  if (r == hipSuccess) r = hipMalloc((void**)&g->d_stp, sizeof(EngineDev*) * replicas);
+  if (r == hipSuccess) r = hipMalloc((void**)&g->d_st, sizeof(EngineDev) * replicas);
+  if (r == hipSuccess) r = hipHostMalloc((void**)&g->h_st, sizeof(EngineDev) * replicas, hipHostMallocDefault);
+  if (r == hipSuccess) r = hipMemcpy(g->d_stp, stp.data(), sizeof(EngineDev*) * replicas, hipMemcpyHostToDevice);
   if (r != hipSuccess) {
     nfsp_group_destroy(g);
     return nfsp::hip_fail(r, "nfsp_group_create");
@@ -800,34 +838,48 @@ extern "C" int nfsp_group_average_ar(nfsp_group* g) {
   return NFSP_OK;
 }
 
+// bump-allocate n items of T in the host / device table pair (8-byte aligned offsets)
+struct TabCursor {
+  size_t off = 0;
+  template <class T>
+  size_t take(size_t n) {
+    const size_t o = (off + 15) & ~(size_t)15;
+    off = o + sizeof(T) * n;
+    return o;
+  }
+};
+
 static int group_update(nfsp_group* g) {
   hipStream_t s = g->ctx->stream;
   const int R = g->R;
   nfsp_engine* e0 = g->eng[0];
   const nfsp_engine_cfg& cfg = e0->cfg;
-  std::vector<EngineDev> h(R);
-  for (int r = 0; r < R; ++r) {
-    NFSP_REQUIRE(g->eng[r]->pending_update, "group replica without a rollout");
-    NFSP_HIP(hipMemcpyAsync(&h[r], g->eng[r]->st, sizeof(EngineDev), hipMemcpyDeviceToHost, s));
-  }
+  for (int r = 0; r < R; ++r) NFSP_REQUIRE(g->eng[r]->pending_update, "group replica without a rollout");
+  // the trigger plans need every replica's insert counts: one gather, one readback
+  k_gather_st<<<1, 256, 0, s>>>(g->d_stp, g->d_st, R);
+  NFSP_LAUNCHED("k_gather_st");
+  NFSP_HIP(hipMemcpyAsync(g->h_st, g->d_st, sizeof(EngineDev) * R, hipMemcpyDeviceToHost, s));
   NFSP_HIP(hipStreamSynchronize(s));
   KTimer kt(e0, KT_LEARNER);
   std::vector<LearnPlan> L(R);
   int rc;
+  int64_t maxU = 0, maxUbr = 0, maxSL = 0;
+  const bool loss_log = e0->log_loss;
   for (int r = 0; r < R; ++r) {
-    g->eng[r]->pending_update = false;
-    if ((rc = plan_update(g->eng[r], h[r], L[r])) != NFSP_OK) return rc;
+    nfsp_engine* e = g->eng[r];
+    NFSP_REQUIRE(e->log_loss == loss_log, "the loss log must be on in all replicas of a group or none");
+    e->pending_update = false;
+    if ((rc = plan_update(e, g->h_st[r], L[r])) != NFSP_OK) return rc;
+    maxU = L[r].maxU > maxU ? L[r].maxU : maxU;
+    maxUbr = L[r].maxUbr > maxUbr ? L[r].maxUbr : maxUbr;
+    maxSL = L[r].maxSL > maxSL ? L[r].maxSL : maxSL;
   }
-  // ---- job tables: the AR chains (2R workgroups, one launch), then per BR round k the
-  // targets and the chain of every (replica, agent) that has a k-th segment
+  // ---- tables: prep / final args per replica; the AR chains (2R workgroups, one launch);
+  // per BR round k the targets and the chain of every (replica, agent) with a k-th segment
   std::vector<ChainJob> ar_jobs;
-  int64_t maxU = 0;
   for (int r = 0; r < R; ++r)
     for (int a = 0; a < 2; ++a)
-      if (L[r].P.A[a].U > 0) {
-        ar_jobs.push_back(ar_job(g->eng[r], L[r], a));
-        maxU = L[r].P.A[a].U > maxU ? L[r].P.A[a].U : maxU;
-      }
+      if (L[r].P.A[a].U > 0) ar_jobs.push_back(ar_job(g->eng[r], L[r], a));
   size_t rounds = 0;
   for (int r = 0; r < R; ++r)
     for (int a = 0; a < 2; ++a) rounds = L[r].seg[a].size() > rounds ? L[r].seg[a].size() : rounds;
@@ -848,9 +900,11 @@ static int group_update(nfsp_group* g) {
   }
   round_off[rounds] = br_jobs.size();
   g->rounds = (int64_t)rounds;
-  const size_t nb_ar = sizeof(ChainJob) * ar_jobs.size(), nb_br = sizeof(ChainJob) * br_jobs.size();
-  const size_t nb_tg = sizeof(TargetJob) * tg_jobs.size();
-  const size_t need = nb_ar + nb_br + nb_tg;
+  TabCursor cur;
+  const size_t o_prep = cur.take<PrepArgs>(R), o_fin = cur.take<FinalArgs>(R);
+  const size_t o_ar = cur.take<ChainJob>(ar_jobs.size()), o_br = cur.take<ChainJob>(br_jobs.size());
+  const size_t o_tg = cur.take<TargetJob>(tg_jobs.size());
+  const size_t need = cur.off;
   if (need > g->tab_cap) {     // every earlier use of the tables completed (the sync above)
     if (g->h_tab) NFSP_HIP(hipHostFree(g->h_tab));
     if (g->d_tab) NFSP_HIP(hipFree(g->d_tab));
@@ -862,28 +916,52 @@ static int group_update(nfsp_group* g) {
     NFSP_HIP(hipMalloc((void**)&g->d_tab, cap));
     g->tab_cap = cap;
   }
-  memcpy(g->h_tab, ar_jobs.data(), nb_ar);
-  memcpy(g->h_tab + nb_ar, br_jobs.data(), nb_br);
-  memcpy(g->h_tab + nb_ar + nb_br, tg_jobs.data(), nb_tg);
-  const ChainJob* d_ar = reinterpret_cast<const ChainJob*>(g->d_tab);
-  const ChainJob* d_br = reinterpret_cast<const ChainJob*>(g->d_tab + nb_ar);
-  const TargetJob* d_tg = reinterpret_cast<const TargetJob*>(g->d_tab + nb_ar + nb_br);
+  for (int r = 0; r < R; ++r) {
+    memcpy(g->h_tab + o_prep + sizeof(PrepArgs) * r, &L[r].P, sizeof(PrepArgs));
+    memcpy(g->h_tab + o_fin + sizeof(FinalArgs) * r, &L[r].F, sizeof(FinalArgs));
+  }
+  memcpy(g->h_tab + o_ar, ar_jobs.data(), sizeof(ChainJob) * ar_jobs.size());
+  memcpy(g->h_tab + o_br, br_jobs.data(), sizeof(ChainJob) * br_jobs.size());
+  memcpy(g->h_tab + o_tg, tg_jobs.data(), sizeof(TargetJob) * tg_jobs.size());
+  const PrepArgs* d_prep = reinterpret_cast<const PrepArgs*>(g->d_tab + o_prep);
+  const FinalArgs* d_fin = reinterpret_cast<const FinalArgs*>(g->d_tab + o_fin);
+  const ChainJob* d_ar = reinterpret_cast<const ChainJob*>(g->d_tab + o_ar);
+  const ChainJob* d_br = reinterpret_cast<const ChainJob*>(g->d_tab + o_br);
+  const TargetJob* d_tg = reinterpret_cast<const TargetJob*>(g->d_tab + o_tg);
   hipEvent_t fork_br = take_event(e0), fork = take_event(e0);
   {
     KTimer kprep(e0, KT_PREP);
-    if (need > 0) NFSP_HIP(hipMemcpyAsync(g->d_tab, g->h_tab, need, hipMemcpyHostToDevice, s));
-    for (int r = 0; r < R; ++r)
-      if ((rc = launch_br_prep(g->eng[r], L[r], s)) != NFSP_OK) return rc;
+    NFSP_HIP(hipMemcpyAsync(g->d_tab, g->h_tab, need, hipMemcpyHostToDevice, s));
+    // the same prep kernels as one engine's, every replica in one launch (blockIdx.z)
+    if (maxUbr > 0) {
+      k_br_prep<1><<<dim3((unsigned)maxUbr, 2, R), 128, 0, s>>>(PrepArgs{}, d_prep);
+      NFSP_LAUNCHED("k_br_prep");
+    }
+    if (loss_log)
+      for (int r = 0; r < R; ++r)
+        for (int a = 0; a < 2; ++a)
+          NFSP_HIP(hipMemsetAsync(g->eng[r]->LB.br_loss + a * g->eng[r]->LB.umax * cfg.epochs, 0xFF,
+                                  sizeof(float) * L[r].P.A[a].U_br * cfg.epochs, s));
     NFSP_HIP(hipEventRecord(fork_br, s));
-    for (int r = 0; r < R; ++r)
-      if ((rc = launch_ar_prep(g->eng[r], L[r], s)) != NFSP_OK) return rc;
+    if (maxSL > 0) {
+      k_ar_slots<1><<<dim3(nfsp_blocks(maxSL, 256), 2, R), 256, 0, s>>>(PrepArgs{}, d_prep);
+      NFSP_LAUNCHED("k_ar_slots");
+    }
+    if (maxU > 0) {
+      k_ar_prep<1><<<dim3((unsigned)maxU, 2, R), 128, 0, s>>>(PrepArgs{}, d_prep);
+      NFSP_LAUNCHED("k_ar_prep");
+    }
+    if (loss_log)
+      for (int r = 0; r < R; ++r)
+        for (int a = 0; a < 2; ++a)
+          NFSP_HIP(hipMemsetAsync(g->eng[r]->LB.ar_loss + a * g->eng[r]->LB.umax * cfg.epochs, 0xFF,
+                                  sizeof(float) * L[r].P.A[a].U * cfg.epochs, s));
     NFSP_HIP(hipEventRecord(fork, s));
-    for (int r = 0; r < R; ++r)
-      if ((rc = launch_res_apply(L[r], s)) != NFSP_OK) return rc;
+    if (maxSL > 0) {
+      k_res_apply<1><<<dim3(nfsp_blocks(maxSL, 256), 2, R), 256, 0, s>>>(PrepArgs{}, d_prep);
+      NFSP_LAUNCHED("k_res_apply");
+    }
   }
-  const bool loss_log = e0->log_loss;
-  for (nfsp_engine* e : g->eng)
-    NFSP_REQUIRE(e->log_loss == loss_log, "the loss log must be on in all replicas of a group or none");
   if (!ar_jobs.empty()) {
     NFSP_HIP(hipStreamWaitEvent(g->s_ar, fork, 0));
     ChainArgs C{};
@@ -917,11 +995,8 @@ static int group_update(nfsp_group* g) {
   }
   e0->pool.push_back(fork);
   e0->pool.push_back(fork_br);
-  for (int r = 0; r < R; ++r) {
-    k_finalize<<<1, 64, 0, s>>>(L[r].F);
-    NFSP_LAUNCHED("k_finalize");
-  }
-  (void)maxU;
+  k_finalize<1><<<R, 64, 0, s>>>(FinalArgs{}, d_fin);
+  NFSP_LAUNCHED("k_finalize");
   return NFSP_OK;
 }
 
@@ -950,8 +1025,7 @@ extern "C" int nfsp_group_step(nfsp_group* g) {
   int rc;
   if ((g->flags & NFSP_GROUP_AVG_AR) && !g->w0_valid)      // common AR nets before the first step
     if ((rc = nfsp_group_average_ar(g)) != NFSP_OK) return rc;
-  for (nfsp_engine* e : g->eng)
-    if ((rc = nfsp::eng::rollout_launch(e)) != NFSP_OK) return rc;
+  if ((rc = nfsp::eng::group_rollout_launch(g->eng.data(), g->R, g->d_roll)) != NFSP_OK) return rc;
   if ((rc = group_update(g)) != NFSP_OK) return rc;
   if (g->flags & NFSP_GROUP_AVG_AR) return nfsp_group_average_ar(g);
   return NFSP_OK;
