@@ -248,6 +248,35 @@ def stub_main(args, world, rank, dist):
         dist.destroy_process_group()
 
 
+def measure_group(pkg, name: str, steps: int, warmup: int) -> dict:
+    """A side measurement beside the headline (N = 1): engine-group config `name` (C3's
+    per-GPU lanes as R learner replicas, on-device AR exchange), W warmup + K un-instrumented
+    steps with the same sync protocol, and the exact exploitability after them."""
+    import torch
+    cfg = CONFIGS[name]
+    R = cfg["replicas"]
+    g = pkg.engine.EngineGroup(R, n_lanes=cfg["n_lanes"] // R, rl_capacity=cfg["rl_capacity"],
+                               sl_capacity=cfg["sl_capacity"], seed=1234, init_seed=0, avg_ar=True)
+    for _ in range(warmup):
+        g.step()
+    torch.cuda.synchronize()
+    s0 = g.stats()
+    el = timed_steps(g.step, steps, 0, None, torch.cuda.synchronize)
+    s1 = g.stats()
+    hands = steps * cfg["n_lanes"]
+    rl = sum(s1["rl_total"]) - sum(s0["rl_total"])
+    out = {"workload": cfg["label"], "learner_replicas": R, "lanes_per_replica": cfg["n_lanes"] // R,
+           "value": hands / el, "unit": "hands/s", "steps": steps, "warmup": warmup,
+           "ms_per_step": el / steps * 1e3, "rl_inserts_per_s": rl / el,
+           "rl_inserts_per_hand": rl / hands,
+           "exploitability_exact_softmax": g.exploitability(0)["exploitability"],
+           "hands_trained": int(s1["hands"])}
+    g.close()
+    del g
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -264,6 +293,9 @@ def main():
                     help="all-reduce of the AR (average-policy) gradient steps once per engine "
                          "step over the ranks (C4; shards.AvgPolicyAllReduce); auto = on for N > 1")
     ap.add_argument("--stub-step-ms", type=float, default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--groups", default="c3_r4,c3_r16,c3_r64",
+                    help="engine-group configs measured beside the C3 headline at N = 1 "
+                         "(`groups` in the JSON line; '' = none)")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -442,6 +474,13 @@ def main():
     out["exploitability_exact"] = {
         "softmax_mixed": ex[0]["exploitability"], "argmax_as_executed": ex[1]["exploitability"],
         "hands_trained_per_gpu": int(s2["hands"]), "unit": "chips (BR_0 + BR_1)"}
+    if world == 1 and args.config == "c3" and args.groups:
+        # several learners on the one GPU (engine groups): new measured configs, not the headline
+        eng.close()
+        del eng
+        torch.cuda.empty_cache()
+        out["groups"] = {name: measure_group(pkg, name, max(args.steps, 10), max(args.warmup, 2))
+                         for name in args.groups.split(",")}
     if rank == 0 and world == 1 and not args.no_cpu:
         threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, threads, cfg)
