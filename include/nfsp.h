@@ -285,6 +285,13 @@ int nfsp_engine_last_update(nfsp_engine* e, int agent, int role, int64_t** dev_r
  * insert order (lane, then play order) -- how a test finds one lane's records in M_RL. */
 int nfsp_engine_lane_counts(nfsp_engine* e, uint32_t** dev_counts);
 
+/* Test hook: from the next nfsp_engine_update on, each agent's AR and BR chains run only the
+ * first max_updates updates of the learner call (0 = all).  Everything else still follows
+ * the full plan: the prep kernels, the reservoir, and the counters and schedules in the
+ * stats.  A test compares the weights with an oracle replay of the same update prefix.  The
+ * engine is not meant to train on after that. */
+int nfsp_engine_set_update_limit(nfsp_engine* e, int64_t max_updates);
+
 /* ---- engine groups: several learners on one GPU ----
  * A group holds R replicas of the engine.  Each replica is an independent
  * main.train (main.py:21-75) over cfg.n_lanes lanes: its own hands, its own M_RL / M_SL, and

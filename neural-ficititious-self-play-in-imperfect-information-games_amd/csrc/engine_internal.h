@@ -221,6 +221,7 @@ struct nfsp_engine {
   bool timing = false;
   bool log_loss = false;
   int64_t last_U[2] = {0, 0}, last_Ubr[2] = {0, 0};   // the last learner call's update counts
+  int64_t update_limit = 0;    // test hook (nfsp_engine_set_update_limit): chains stop after this many
   std::vector<hipEvent_t> pool;
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> marks;
 };

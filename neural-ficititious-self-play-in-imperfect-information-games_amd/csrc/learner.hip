@@ -540,6 +540,14 @@ int plan_update(nfsp_engine* e, const EngineDev& h, LearnPlan& L) {
       it += 2;
       eps = (cfg.quirks & NFSP_EXT_EPS_CONST) ? cfg.epsilon : eps / (double)it;
     }
+    if (e->update_limit > 0) {         // test hook: only a prefix of the updates runs
+      std::vector<Segment> kept;
+      for (const Segment& sg : L.seg[a]) {
+        if (sg.u >= e->update_limit) break;
+        kept.push_back(sg.v <= e->update_limit ? sg : Segment{sg.u, e->update_limit, false});
+      }
+      L.seg[a] = kept;
+    }
     F.iteration[a] = it;
     F.tcount[a] = tc;
     F.syncs[a] = syncs;
@@ -599,6 +607,7 @@ ChainJob ar_job(const nfsp_engine* e, const LearnPlan& L, int a) {
   j.loss_out = e->log_loss ? e->LB.ar_loss + a * um * e->cfg.epochs : nullptr;
   j.u0 = 0;
   j.u1 = L.P.A[a].U;
+  if (e->update_limit > 0 && j.u1 > e->update_limit) j.u1 = e->update_limit;   // test hook
   return j;
 }
 
@@ -997,6 +1006,12 @@ static int group_update(nfsp_group* g) {
   e0->pool.push_back(fork_br);
   k_finalize<1><<<R, 64, 0, s>>>(FinalArgs{}, d_fin);
   NFSP_LAUNCHED("k_finalize");
+  return NFSP_OK;
+}
+
+extern "C" int nfsp_engine_set_update_limit(nfsp_engine* e, int64_t max_updates) {
+  NFSP_REQUIRE(e && max_updates >= 0, "bad argument");
+  e->update_limit = max_updates;
   return NFSP_OK;
 }
 

@@ -167,6 +167,11 @@ class SelfPlayEngine:
         c = c.astype(np.int64) & 0xFFFF
         return np.stack([(c >> (4 * k)) & 15 for k in range(4)], axis=1)
 
+    def set_update_limit(self, max_updates: int):
+        """Test hook (nfsp_engine_set_update_limit): the chains run only a prefix of each
+        learner call's updates."""
+        native.check(self.L.nfsp_engine_set_update_limit(self.h, int(max_updates)), "set_update_limit")
+
     loss_log = False
 
     def set_loss_log(self, on=True):

@@ -103,6 +103,7 @@ SIGNATURES = {
     "nfsp_engine_losses": (I32, [P, P]),
     "nfsp_engine_set_timing": (I32, [P, I32]),
     "nfsp_engine_get_timings": (I32, [P, C.POINTER(F64), C.POINTER(I64)]),
+    "nfsp_engine_set_update_limit": (I32, [P, I64]),
     "nfsp_group_create": (I32, [P, C.POINTER(EngineCfg), I32, U32, C.POINTER(P)]),
     "nfsp_group_destroy": (I32, [P]),
     "nfsp_group_engine": (I32, [P, I32, C.POINTER(P)]),

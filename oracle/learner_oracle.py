@@ -109,7 +109,7 @@ def bits_to_x(bits):
     return ((bits[:, None] >> np.arange(30)) & 1).astype(np.float32)
 
 
-def learner_step(cfg, state, quirks=7):
+def learner_step(cfg, state, quirks=7, max_updates=None, trace=None):
     """Replay nfsp_engine_update.
 
     cfg: dict(c, batch, epochs, rl_capacity, sl_capacity, target_every, lr_br, lr_ar, gamma,
@@ -122,6 +122,9 @@ def learner_step(cfg, state, quirks=7):
       * pend_x, pend_a, pend_pos: the rollout's SL inserts.
     Returns per agent: weights, iteration, epsilon, lr_br, temp, exploitability (last BR
     proxy), br_updates, ar_updates, reservoir (bits, a) after the update.
+    max_updates: replay only the first max_updates BR and AR updates of each agent (the
+    engine's nfsp_engine_set_update_limit); the counters still follow the full plan.
+    trace(a, net, u, flat_weights): called after each replayed update u (net 0 = AR, 1 = BR).
     """
     c, B, E = cfg["c"], cfg["batch"], cfg["epochs"]
     k0, k1 = cfg["seed"] & M32, (cfg["seed"] >> 32) & M32
@@ -142,8 +145,9 @@ def learner_step(cfg, state, quirks=7):
         it, tc, eps = st["iteration"], st["br_updates"], st["epsilon"]
         it0 = it
         expl = None
+        lim = lambda n: n if max_updates is None else min(n, max_updates)
         # ---- BR updates
-        for u in range(U_br):
+        for u in range(lim(U_br)):
             m = m_br0 + u
             pm = m * c
             win = min(pm, cfg["rl_capacity"])
@@ -164,6 +168,11 @@ def learner_step(cfg, state, quirks=7):
             br.fit(s, target, lr, epochs=E, perms=perms)
             if (tc + u) % cfg["target_every"] == 0:
                 tg.set_weights(br.get_weights())
+            if trace is not None:
+                trace(a, 1, u, br.flat())
+            it += 2
+            eps = cfg["epsilon"] if quirks & EXT_EPS_CONST else eps / it
+        for u in range(lim(U_br), U_br):      # schedules of updates past the prefix
             it += 2
             eps = cfg["epsilon"] if quirks & EXT_EPS_CONST else eps / it
         # ---- AR updates, the reservoir as of each trigger
@@ -172,6 +181,10 @@ def learner_step(cfg, state, quirks=7):
         cap = cfg["sl_capacity"]
         slots = reservoir_slots(a, sl0, n_sl, cap, k0, k1, quirks)
         pos = np.asarray(st["pend_pos"][:n_sl], np.int64)
+        # each slot's inserts of this rollout in insert order: the latest one before a
+        # trigger is a bisection (slot contents as of the trigger)
+        order = np.argsort(slots, kind="stable")
+        ss = slots[order]
         n_ar = 0
         for u in range(U):
             m = m_first + u
@@ -181,18 +194,24 @@ def learner_step(cfg, state, quirks=7):
             if count <= B:
                 continue
             n_ar += 1
+            if u >= lim(U):
+                continue
             picks = sample_distinct(B, 0, count, TAG_SAMPLE | (a * 2), m, k0, k1)
             xb = np.empty(B, np.int64)
             ya = np.empty((B, 3), np.float32)
             for b, j in enumerate(picks):
-                hit = np.nonzero(slots[:nb] == j)[0]
-                if len(hit):
-                    q = hit[-1]
+                lo, hi = np.searchsorted(ss, j, side="left"), np.searchsorted(ss, j, side="right")
+                qs = order[lo:hi]                           # this slot's inserts, ascending
+                k = int(np.searchsorted(qs, nb, side="left"))
+                if k:
+                    q = qs[k - 1]
                     xb[b], ya[b] = st["pend_x"][q], st["pend_a"][q]
                 else:
                     xb[b], ya[b] = st["sl_s_bits"][j], st["sl_a"][j]
             perms = np.stack([draw_perm(B, e, TAG_PERM | (a * 2), m, k0, k1) for e in range(E)])
             ar.fit(bits_to_x(xb), ya, np.float32(cfg["lr_ar"]), epochs=E, perms=perms)
+            if trace is not None:
+                trace(a, 0, u, ar.flat())
         # ---- the reservoir after the rollout's inserts (last writer per slot)
         res_x = np.array(st["sl_s_bits"], np.int64).copy()
         res_a = np.array(st["sl_a"], np.float32).copy()
