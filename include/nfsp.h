@@ -120,6 +120,24 @@ int nfsp_num_envs(const nfsp_ctx* ctx);
  * host's MT19937 stream (nfsp_amd.pyrandom.set_python_semantics(3 | 2)), drawn on the host
  * and injected here. */
 int nfsp_env_set_deal(nfsp_ctx* ctx, const uint8_t* dev_ranks /* [n,3] */);
+/* Deal modes (SURVEY §8(b) deal_mode) of nfsp_env_reset.  The reference reshuffles a fresh
+ * 6-card deck with the global `random` at every Env.reset (leduc/deck.py:42-44) and pops
+ * P0, P1 and the public card from its end.
+ *   PHILOX  (default): the device draw keyed by (ctx seed, env, reset index);
+ *   PY3_MT / PY2_MT:   that shuffle on the host, under CPython 3's / 2.7's random seeded
+ *                      with random.seed(seed).  Every reset deals env 0, 1, ..., n-1 from
+ *                      the one stream, and the deck is its only consumer.  The drop-in
+ *                      Python Env shares the process's global random with the rest of
+ *                      main.train instead (nfsp_amd.pyrandom).  Leduc only.
+ * A pending nfsp_env_set_deal still takes precedence for the next reset. */
+#define NFSP_DEAL_PHILOX 0
+#define NFSP_DEAL_PY3_MT 1
+#define NFSP_DEAL_PY2_MT 2
+int nfsp_env_set_deal_mode(nfsp_ctx* ctx, int mode, uint64_t seed);
+/* Host only (no device work): the first n deals (P0, P1, public rank) of deal mode PY3_MT or
+ * PY2_MT from random.seed(seed), as nfsp_env_reset would draw them for n consecutive resets
+ * of a 1-env ctx. */
+int nfsp_deal_mt(int mode, uint64_t seed, int64_t n, uint8_t* out /* [n,3] */);
 /* Env.reset(dealer) (leduc/newenv.py:76-114) for every env.  Deal = the pending
  * nfsp_env_set_deal if any, else a Philox draw keyed by (seed, env, reset index). */
 int nfsp_env_reset(nfsp_ctx* ctx, const uint8_t* dev_dealer /* [n] */);

@@ -136,6 +136,7 @@ extern "C" int nfsp_destroy(nfsp_ctx* c) {
   if (!c) return NFSP_OK;
   if (c->hands) (void)hipFree(c->hands);
   if (c->pending_deal) (void)hipFree(c->pending_deal);
+  nfsp::deal_mt_free(c);
   if (c->scratch_f64) (void)hipFree(c->scratch_f64);
   if (c->scratch_i64) (void)hipFree(c->scratch_i64);
   delete c;
@@ -169,6 +170,10 @@ extern "C" int nfsp_env_set_deal(nfsp_ctx* c, const uint8_t* ranks) {
 
 extern "C" int nfsp_env_reset(nfsp_ctx* c, const uint8_t* dealer) {
   NFSP_REQUIRE(c && dealer, "null argument");
+  if (c->deal_mt && !c->has_pending_deal) {       // nfsp_env_set_deal_mode: CPython's shuffle
+    const int rc = nfsp::deal_mt_stage(c);
+    if (rc != NFSP_OK) return rc;
+  }
   const uint64_t ri = c->resets++;
   k_env_reset<<<nfsp_blocks(c->n_envs, 256), 256, 0, c->stream>>>(
       c->hands, c->n_envs, dealer, c->has_pending_deal ? c->pending_deal : nullptr,

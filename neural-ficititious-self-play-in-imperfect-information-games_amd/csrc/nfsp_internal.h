@@ -22,6 +22,7 @@ struct nfsp_ctx {
   double* scratch_f64 = nullptr;      // small device scratch
   int64_t* scratch_i64 = nullptr;     // insert de-duplication scratch
   int64_t scratch_i64_cap = 0;
+  void* deal_mt = nullptr;            // nfsp_env_set_deal_mode's MT19937 state (deal_mt.hip)
 };
 
 namespace nfsp {
@@ -29,6 +30,8 @@ namespace nfsp {
 void set_error(const std::string& msg);
 int fail(int code, const std::string& msg);
 int hip_fail(hipError_t e, const char* what);
+int deal_mt_stage(nfsp_ctx* c);       // MT deal modes: the next reset's deals -> pending_deal
+void deal_mt_free(nfsp_ctx* c);
 
 }  // namespace nfsp
 

@@ -75,6 +75,8 @@ SIGNATURES = {
     "nfsp_num_envs": (I32, [P]),
     "nfsp_env_set_deal": (I32, [P, P]),
     "nfsp_env_reset": (I32, [P, P]),
+    "nfsp_env_set_deal_mode": (I32, [P, I32, U64]),
+    "nfsp_deal_mt": (I32, [I32, U64, I64, P]),
     "nfsp_env_get_state": (I32, [P, I32, P, P, P, P, P, P]),
     "nfsp_env_step": (I32, [P, P, I32, P, P]),
     "nfsp_env_round": (I32, [P, P]),
@@ -114,6 +116,7 @@ SIGNATURES = {
     "nfsp_group_rounds": (I32, [P, C.POINTER(I64)]),
 }
 GROUP_AVG_AR = 1
+DEAL_PHILOX, DEAL_PY3_MT, DEAL_PY2_MT = 0, 1, 2
 GROUP_MAX_REPLICAS = 64
 
 _LIB = None

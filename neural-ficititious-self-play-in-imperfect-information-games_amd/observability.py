@@ -64,3 +64,30 @@ def engine_scalars(eng, exact: bool = False) -> dict:
         for m, tag in ((0, "softmax"), (1, "argmax")):
             out[f"exploitability_exact_{tag}"] = eng.exploitability(m)["exploitability"]
     return out
+
+
+def save_curve(points, csv_path: str, png_path: str | None = None, ylabel: str = "exploitability proxy",
+               xlabel: str = "hands") -> None:
+    """The curve main.train plots at its end (main.py:122-123: plt.plot(plotter)), as a CSV
+    artefact and, when matplotlib is importable, a PNG (Agg backend, no display).  `points`:
+    a sequence of (x, y) pairs or plain y values (x = their index, as plt.plot(plotter))."""
+    pts = [(i, p) if not isinstance(p, (tuple, list)) else tuple(p) for i, p in enumerate(points)]
+    with open(csv_path, "w") as f:
+        f.write(f"{xlabel},{ylabel}\n")
+        for x, y in pts:
+            f.write(f"{x},{float(y)!r}\n")
+    if png_path is None:
+        return
+    try:
+        import matplotlib
+        matplotlib.use("Agg")
+        import matplotlib.pyplot as plt
+    except ImportError:
+        return
+    fig, ax = plt.subplots(figsize=(6, 4))
+    ax.plot([p[0] for p in pts], [p[1] for p in pts])
+    ax.set_xlabel(xlabel)
+    ax.set_ylabel(ylabel)
+    fig.tight_layout()
+    fig.savefig(png_path, dpi=100)
+    plt.close(fig)

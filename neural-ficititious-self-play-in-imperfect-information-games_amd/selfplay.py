@@ -38,8 +38,10 @@ def play_hand(env, players, dealer, eta):
     return policy
 
 
-def train(env, player1, player2, episodes=400000, eta=0.1, stats_every=100):
-    """Returns the exploitability-proxy curve main.train plots (main.py:73-75,122)."""
+def train(env, player1, player2, episodes=400000, eta=0.1, stats_every=100, plot: str | None = None):
+    """Returns the exploitability-proxy curve main.train plots (main.py:73-75,122).  `plot`:
+    a path prefix; the curve is written to <plot>.csv and <plot>.png (main.py:122-123 shows
+    it with plt.show() instead)."""
     players = [player1, player2]
     dealer = pyrandom.randint(0, 1)
     curve = []
@@ -50,6 +52,9 @@ def train(env, player1, player2, episodes=400000, eta=0.1, stats_every=100):
             for pl in players:
                 pl.sampled_actions()
             curve.append(players[0].average_payoff_br() + players[1].average_payoff_br())
+    if plot:
+        from .observability import save_curve
+        save_curve(curve, plot + ".csv", plot + ".png", xlabel="report")
     return curve
 
 

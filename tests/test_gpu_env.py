@@ -115,3 +115,21 @@ def test_dropin_do_action_matches_reference_kat(pkg):
         return (int(h["hist"]) & 0xFFFFFF, (int(h["c0"]), int(h["c1"])),
                 (int(h["raises0"]), int(h["raises1"])), int(h["slot"]), h["la"][p])
     assert _replay_do_action(make, state) == 1720
+
+
+@pytest.mark.gpu
+def test_env_reset_mt_deal_mode_deals_like_the_reference(pkg):
+    """nfsp_env_set_deal_mode(PY3_MT, seed): nfsp_env_reset deals env 0..n-1 of every reset
+    from CPython 3's shuffle of random.seed(seed) -- the reference's deals (deal_seq.npz)."""
+    ref = golden("deal_seq.npz")["seed7"]
+    n = 500
+    ctx = pkg.native.Context(n)
+    ctx.call("nfsp_env_set_deal_mode", pkg.native.DEAL_PY3_MT, 7)
+    dealer = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    hb = torch.zeros(n * 64, dtype=torch.uint8, device="cuda")
+    for k in range(4):
+        ctx.call("nfsp_env_reset", pkg.native.ptr(dealer))
+        ctx.call("nfsp_env_export", pkg.native.ptr(hb))
+        torch.cuda.synchronize()
+        ranks = hb.view(n, 64)[:, 48:51].cpu().numpy()
+        assert np.array_equal(ranks, ref[k * n:(k + 1) * n]), k

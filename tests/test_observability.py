@@ -31,3 +31,15 @@ def test_engine_scalars_tags(pkg):
         assert sc[f"Player{a}/folds"] + sc[f"Player{a}/calls"] + sc[f"Player{a}/raises"] > 0
     assert sc["hands"] == 3 * 4096
     assert sc["exploitability_exact_softmax"] >= 0
+
+
+def test_save_curve_csv_and_png(pkg, tmp_path):
+    """The curve artefact main.train plots at its end (main.py:122-123): CSV + PNG."""
+    obs = pkg.observability
+    obs.save_curve([1.5, 1.25, 1.0], str(tmp_path / "c.csv"), str(tmp_path / "c.png"))
+    lines = (tmp_path / "c.csv").read_text().splitlines()
+    assert lines[0] == "hands,exploitability proxy" and lines[1:] == ["0,1.5", "1,1.25", "2,1.0"]
+    pytest.importorskip("matplotlib")
+    assert (tmp_path / "c.png").read_bytes()[:8] == b"\x89PNG\r\n\x1a\n"
+    obs.save_curve([(128, 2.0), (256, 1.75)], str(tmp_path / "d.csv"))
+    assert (tmp_path / "d.csv").read_text().splitlines()[1:] == ["128,2.0", "256,1.75"]

@@ -7,6 +7,7 @@ Python 2 in the image, so mode 2 is checked against that published algorithm dra
 """
 import random
 
+import numpy as np
 import pytest
 
 
@@ -92,3 +93,33 @@ def test_dropin_deck_deals_like_the_reference(pkg):
     assert c.rank == 0 and str(c) == "Ace Spades 0 1"
     assert pkg.deck.Deck().fake_pub_card().rank == -1
     assert len(pkg.deck.Deck()._cards) == 6
+
+
+def test_capi_mt_deals_match_the_reference(pkg):
+    """The C-ABI's host MT19937 deals (nfsp_deal_mt, the engine of nfsp_env_set_deal_mode):
+    PY3_MT against the reference's own deals (deal_seq.npz, 3 seeds x 2,000 resets), PY2_MT
+    against the CPython 2.7 shuffle restated in nfsp_amd.pyrandom.  Host code only: no GPU."""
+    import ctypes as C
+    from conftest import golden
+    L = pkg.native.load()
+    for seed in (1234, 7, 99):
+        ref = golden("deal_seq.npz")[f"seed{seed}"]
+        out = np.zeros((len(ref), 3), np.uint8)
+        assert L.nfsp_deal_mt(pkg.native.DEAL_PY3_MT, seed, len(ref), out.ctypes.data_as(C.c_void_p)) == 0
+        assert np.array_equal(out, ref), seed
+    pr = pkg.pyrandom
+    for seed in (0, 5, 2 ** 40 + 3):
+        out = np.zeros((300, 3), np.uint8)
+        assert L.nfsp_deal_mt(pkg.native.DEAL_PY2_MT, seed, 300, out.ctypes.data_as(C.c_void_p)) == 0
+        pr.set_python_semantics(2)
+        try:
+            random.seed(seed)
+            want = []
+            for _ in range(300):
+                cards = list(range(6))
+                pr.shuffle(cards)
+                want.append((cards[5] >> 1, cards[4] >> 1, cards[3] >> 1))
+        finally:
+            pr.set_python_semantics(3)
+        assert np.array_equal(out, np.array(want, np.uint8)), seed
+    assert L.nfsp_deal_mt(0, 1, 1, out.ctypes.data_as(C.c_void_p)) != 0     # PHILOX: refused

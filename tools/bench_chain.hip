@@ -25,8 +25,16 @@ int fail(int code, const std::string&) { return code; }
 int hip_fail(hipError_t, const char*) { return NFSP_EHIP; }
 namespace eng {
 hipEvent_t take_event(nfsp_engine*) { return nullptr; }
+int engine_create(nfsp_ctx*, const nfsp_engine_cfg*, bool, nfsp_engine**) { return NFSP_EINVAL; }
+int group_rollout_table(nfsp_engine* const*, int, void**) { return NFSP_EINVAL; }
+int group_rollout_launch(nfsp_engine* const*, int, const void*) { return NFSP_EINVAL; }
 }
 }
+namespace nfsp { namespace chain {
+int launch_chain_br_linear(const ChainArgs&, int, bool, hipStream_t) { return NFSP_EINVAL; }
+} }
+extern "C" int nfsp_engine_destroy(nfsp_engine*) { return NFSP_OK; }
+extern "C" int nfsp_engine_get_timings(nfsp_engine*, double*, int64_t*) { return NFSP_OK; }
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); exit(1);} } while (0)
 
@@ -88,8 +96,9 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&dw2, w.size() * 4));
   CK(hipMemcpy(dw2, w.data(), w.size() * 4, hipMemcpyHostToDevice));
   ChainArgs C{};
-  C.w[0] = dw; C.rec = drec; C.umax = U; C.u0[0] = 0; C.u1[0] = U; C.B = B; C.E = E; C.stamps = dst;
-  C.w[1] = dw2; C.u0[1] = 0; C.u1[1] = U;            // second chain: same records, own weights
+  C.job[0].w = dw; C.job[0].rec = drec; C.job[0].u0 = 0; C.job[0].u1 = U; C.B = B; C.E = E; C.stamps = dst;
+  C.job[1] = C.job[0];
+  C.job[1].w = dw2;                                  // second chain: same records, own weights
   chainref::RefArgs R{};
   R.w[0] = dw; R.fit = dfit; R.umax = U; R.u0[0] = 0; R.u1[0] = U; R.B = B; R.E = E;
   R.lr_fixed = 0.1f; R.lr0 = 0.05;
