@@ -73,6 +73,10 @@ CONFIGS = {
        for R in (2, 4, 8, 16, 32, 64)},
     "c5": dict(n_lanes=1_048_576, rl_capacity=200_000, sl_capacity=2_000_000, game="kuhn",
                label="C5: Kuhn swap-in, 1,048,576 lanes/GPU, C3's memories and cadence"),
+    # C5's exploitability -> 0 check runs textbook NFSP with the MSE Q loss
+    "c5_tb": dict(n_lanes=1_048_576, rl_capacity=200_000, sl_capacity=2_000_000, game="kuhn", quirks=504,
+                  label="C5: Kuhn swap-in, 1,048,576 lanes/GPU, C3's memories and cadence, "
+                        "textbook NFSP with the MSE Q loss (quirks NFSP_TEXTBOOK_MSE)"),
 }
 
 PEAK_FP32_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA peak
@@ -321,9 +325,10 @@ def main():
                                      sl_capacity=cfg["sl_capacity"], seed=1234 + R * rank,
                                      init_seed=R * rank, game=game, avg_ar=True)
     else:
+        extra = {"quirks": cfg["quirks"]} if "quirks" in cfg else {}
         eng = pkg.engine.SelfPlayEngine(n_lanes=cfg["n_lanes"], rl_capacity=cfg["rl_capacity"],
                                         sl_capacity=cfg["sl_capacity"], seed=1234 + rank,
-                                        init_seed=rank, game=game)
+                                        init_seed=rank, game=game, **extra)
     avg = None
     if R == 1 and dist is not None and (args.ar_allreduce == "on" or (args.ar_allreduce == "auto" and world > 1)):
         # C4: the AR nets of both agents, averaged over the ranks once per engine step

@@ -80,8 +80,17 @@ extern "C" {
                                      for its k-th AR decision) and passes the one-hot vector:
                                      the reference passes the softmax itself, which the env
                                      executes as its argmax (agent/agent.py:143, newenv.py:135) */
+#define NFSP_EXT_MSE_Q 256u       /* with NFSP_EXT_LINEAR_Q: the BR / target nets are fitted with
+                                     mean squared error, not the reference's Huber loss
+                                     (agent/agent.py:91-99).  Huber's clipped gradient makes Q a
+                                     robust location estimate (between median and mean), so with
+                                     bimodal returns (a +-2 showdown) Q(s, a) sits up to ~1 chip from
+                                     the expected return and the greedy "best response" is not one
+                                     (tests/studies/kuhn_diag.py).  Requires LINEAR_Q. */
 #define NFSP_TEXTBOOK (NFSP_EXT_SL_ONEHOT | NFSP_EXT_RESERVOIR | NFSP_EXT_LINEAR_Q | \
                        NFSP_EXT_EPS_CONST | NFSP_EXT_SAMPLE_AR)
+/* NFSP_TEXTBOOK with the expected-return (MSE) Q loss: NFSP as Heinrich & Silver train it */
+#define NFSP_TEXTBOOK_MSE (NFSP_TEXTBOOK | NFSP_EXT_MSE_Q)
 
 typedef struct nfsp_ctx nfsp_ctx;
 

@@ -171,7 +171,8 @@ __device__ inline floatx4 mfma3t(bf16x8 ahi, bf16x8 amid, bf16x8 alo, bf16x8 b) 
 }
 
 // RELU: 0 = the AR net (softmax, categorical cross-entropy), 1 = the BR net (ReLU Q head,
-// Huber), 2 = a BR net with a linear Q head (NFSP_EXT_LINEAR_Q, Huber).
+// Huber), 2 = a BR net with a linear Q head (NFSP_EXT_LINEAR_Q, Huber), 3 = linear head with
+// mean squared error (NFSP_EXT_MSE_Q).
 // TABLE: the workgroups' jobs come from the device table C.jobs (engine groups); else from
 // the kernel arguments (C.job, one engine) -- a separate instantiation, so the one-engine
 // chain's code is not touched by the group's
@@ -315,10 +316,10 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
         float dd[3];
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-          const float ee = tt[k] - (RELU == 2 ? oz[k] : fmaxf(oz[k], 0.f));
-          // |e| > 1 ? sign(e) : e  ==  clamp(e, -1, 1)
-          const float gg = __builtin_amdgcn_fmed3f(ee, -1.f, 1.f);
-          dd[k] = (RELU == 2 || oz[k] > 0.f) ? gg * -inv3m : 0.f;
+          const float ee = tt[k] - (RELU >= 2 ? oz[k] : fmaxf(oz[k], 0.f));
+          // Huber: |e| > 1 ? sign(e) : e  ==  clamp(e, -1, 1); MSE (RELU 3): 2 e
+          const float gg = RELU == 3 ? ee * 2.0f : __builtin_amdgcn_fmed3f(ee, -1.f, 1.f);
+          dd[k] = (RELU >= 2 || oz[k] > 0.f) ? gg * -inv3m : 0.f;
         }
         d0 = dd[0]; d1 = dd[1]; d2 = dd[2];
       } else {
@@ -352,10 +353,10 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
     if (LOSS) {            // fit loss of this minibatch (before its update), Keras' epoch mean
       float Ls;
       if (RELU) {          // huber_loss with py2's 1 / 2 == 0: |e| > 1 ? |e| : e^2 / 2, mean over 3
-        float acc = 0.f;
+        float acc = 0.f;   // (RELU 3: e^2)
         for (int k = 0; k < 3; ++k) {
-          const float e = tt_keep[k] - (RELU == 2 ? o_keep[k] : fmaxf(o_keep[k], 0.f));
-          acc += fabsf(e) > 1.0f ? fabsf(e) : 0.5f * e * e;
+          const float e = tt_keep[k] - (RELU >= 2 ? o_keep[k] : fmaxf(o_keep[k], 0.f));
+          acc += RELU == 3 ? e * e : (fabsf(e) > 1.0f ? fabsf(e) : 0.5f * e * e);
         }
         Ls = acc * (1.0f / 3.0f);
       } else {             // categorical cross-entropy: -sum t log(clip(y / S))
@@ -530,7 +531,7 @@ int launch_chain(const ChainArgs& C, int blocks, bool loss_log, hipStream_t s, s
 // AR chain launcher (chain_ar.hip): k_chain3<0, loss_log, *> on `s`, `blocks` workgroups.
 int launch_chain_ar(const ChainArgs& C, int blocks, bool loss_log, hipStream_t s);
 // BR chain with a linear Q head (NFSP_EXT_LINEAR_Q; chain_brlin.hip): k_chain3<2, loss_log>.
-int launch_chain_br_linear(const ChainArgs& C, int blocks, bool loss_log, hipStream_t s);
+int launch_chain_br_linear(const ChainArgs& C, int blocks, bool loss_log, bool mse, hipStream_t s);
 
 }  // namespace chain
 }  // namespace nfsp

@@ -7,8 +7,9 @@
 namespace nfsp {
 namespace chain {
 
-int launch_chain_br_linear(const ChainArgs& C, int blocks, bool loss_log, hipStream_t s) {
-  static std::atomic<uint64_t> attr{0};
+int launch_chain_br_linear(const ChainArgs& C, int blocks, bool loss_log, bool mse, hipStream_t s) {
+  static std::atomic<uint64_t> attr{0}, attr_mse{0};
+  if (mse) return launch_chain<3>(C, blocks, loss_log, s, attr_mse);   // NFSP_EXT_MSE_Q
   return launch_chain<2>(C, blocks, loss_log, s, attr);
 }
 

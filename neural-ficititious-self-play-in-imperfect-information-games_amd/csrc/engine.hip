@@ -510,8 +510,10 @@ int engine_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, bool own_streams, n
   NFSP_REQUIRE(cfg->sl_capacity < (1ll << 31), "sl_capacity must be < 2^31");
   NFSP_REQUIRE(cfg->rl_capacity < (1ll << 40), "rl_capacity too large");
   NFSP_REQUIRE(cfg->inserts_per_update >= 1 && cfg->target_every >= 1, "bad cadence");
-  NFSP_REQUIRE((cfg->quirks & ~(NFSP_QUIRKS_REFERENCE | NFSP_TEXTBOOK)) == 0,
+  NFSP_REQUIRE((cfg->quirks & ~(NFSP_QUIRKS_REFERENCE | NFSP_TEXTBOOK_MSE)) == 0,
                "unknown bits in quirks (NFSP_QUIRK_* | NFSP_EXT_*)");
+  NFSP_REQUIRE(!(cfg->quirks & NFSP_EXT_MSE_Q) || (cfg->quirks & NFSP_EXT_LINEAR_Q),
+               "NFSP_EXT_MSE_Q requires NFSP_EXT_LINEAR_Q");
   *out = nullptr;
   nfsp_engine* e = new nfsp_engine();
   e->ctx = ctx;

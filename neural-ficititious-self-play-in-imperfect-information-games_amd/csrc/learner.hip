@@ -640,7 +640,8 @@ ChainJob br_chain_job(const nfsp_engine* e, int a, const Segment& sg) {
 }
 
 int launch_br_chain(const ChainArgs& C, int blocks, unsigned quirks, bool loss_log, hipStream_t s) {
-  if (quirks & NFSP_EXT_LINEAR_Q) return launch_chain_br_linear(C, blocks, loss_log, s);
+  if (quirks & NFSP_EXT_LINEAR_Q)
+    return launch_chain_br_linear(C, blocks, loss_log, (quirks & NFSP_EXT_MSE_Q) != 0, s);
   static std::atomic<uint64_t> attr{0};
   return launch_chain<1>(C, blocks, loss_log, s, attr);
 }

@@ -21,6 +21,8 @@ QUIRKS_REFERENCE = 7
 # textbook-NFSP extensions (include/nfsp.h NFSP_EXT_*; not the reference's algorithm)
 EXT_SL_ONEHOT, EXT_RESERVOIR, EXT_LINEAR_Q, EXT_EPS_CONST, EXT_SAMPLE_AR = 8, 16, 32, 64, 128
 TEXTBOOK = EXT_SL_ONEHOT | EXT_RESERVOIR | EXT_LINEAR_Q | EXT_EPS_CONST | EXT_SAMPLE_AR
+EXT_MSE_Q = 256
+TEXTBOOK_MSE = TEXTBOOK | EXT_MSE_Q
 
 P = C.c_void_p
 I32, I64, U32, U64, F32, F64 = C.c_int, C.c_int64, C.c_uint, C.c_uint64, C.c_float, C.c_double

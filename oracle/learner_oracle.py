@@ -85,6 +85,7 @@ def draw_perm(batch, e, stream, m, k0, k1):
 
 
 EXT_RESERVOIR, EXT_LINEAR_Q, EXT_EPS_CONST = 16, 32, 64      # include/nfsp.h NFSP_EXT_*
+EXT_MSE_Q = 256
 
 
 def reservoir_slots(a, sl_total0, n_sl, cap, k0, k1, ext=0):
@@ -139,7 +140,8 @@ def learner_step(cfg, state, quirks=7, max_updates=None, trace=None):
         U_br = max(0, m_last - m_br0 + 1)
         log_cap = len(st["rl_s_bits"])
         ar = nn.MLP(nn.ACT_SOFTMAX, 64, weights=nn.unpack_weights(st["w"][0]))
-        br_act = nn.ACT_LINEAR if quirks & EXT_LINEAR_Q else nn.ACT_RELU
+        br_act = (nn.ACT_LINEAR_MSE if quirks & EXT_MSE_Q else nn.ACT_LINEAR) if quirks & EXT_LINEAR_Q \
+            else nn.ACT_RELU
         br = nn.MLP(br_act, 64, weights=nn.unpack_weights(st["w"][1]))
         tg = nn.MLP(br_act, 64, weights=nn.unpack_weights(st["w"][2]))
         it, tc, eps = st["iteration"], st["br_updates"], st["epsilon"]

@@ -36,6 +36,7 @@ N_IN, N_OUT = 30, 3
 ACT_RELU = 0              # BR / target-BR output activation (agent/agent.py:103)
 ACT_SOFTMAX = 1           # AR output activation (agent/agent.py:112)
 ACT_LINEAR = 2            # BR head under the engine's NFSP_EXT_LINEAR_Q (not the reference)
+ACT_LINEAR_MSE = 3        # ... with NFSP_EXT_MSE_Q: the same head, Keras mean_squared_error
 
 
 def glorot_uniform(rng: np.random.RandomState, fan_in: int, fan_out: int) -> np.ndarray:
@@ -98,7 +99,7 @@ class MLP:
         z2 = dense_seq(h, self.W2, self.b2)
         if self.act == ACT_RELU:
             y = np.maximum(z2, F32(0))
-        elif self.act == ACT_LINEAR:
+        elif self.act in (ACT_LINEAR, ACT_LINEAR_MSE):
             y = z2
         else:
             y = softmax3(z2)
@@ -122,6 +123,10 @@ class MLP:
             dldy = np.where(np.abs(e) > F32(1.0), np.sign(e), e).astype(F32)
             dldy = -dldy / F32(3 * m)
             dz2 = dldy * (z2 > 0).astype(F32) if self.act == ACT_RELU else dldy
+        elif self.act == ACT_LINEAR_MSE:
+            # mean_squared_error: mean over the 3 outputs of e^2, then over the batch
+            e = t2d - y
+            dz2 = (-(e * F32(2.0)) / F32(3 * m)).astype(F32)
         else:
             # categorical_crossentropy, TF backend, from_logits=False.
             S = y.sum(axis=-1, keepdims=True)
@@ -152,6 +157,8 @@ class MLP:
             e = t - y
             v = np.where(np.abs(e) > 1.0, np.abs(e), 0.5 * e * e)
             return float(v.mean(axis=-1).mean())
+        if self.act == ACT_LINEAR_MSE:
+            return float(((t - y) ** 2).mean(axis=-1).mean())
         p = y / y.sum(axis=-1, keepdims=True)
         pc = np.clip(p, float(CE_EPS), 1.0 - float(CE_EPS))
         return float((-(t * np.log(pc)).sum(axis=-1)).mean())

@@ -221,7 +221,9 @@ def test_device_views_keep_the_engine_alive(pkg):
 
 def test_engine_rejects_unknown_quirk_bits(pkg):
     with pytest.raises(pkg.native.NativeError, match="unknown bits"):
-        pkg.engine.SelfPlayEngine(n_lanes=64, quirks=256)
-    eng = pkg.engine.SelfPlayEngine(n_lanes=64, quirks=pkg.native.QUIRKS_REFERENCE | pkg.native.TEXTBOOK)
+        pkg.engine.SelfPlayEngine(n_lanes=64, quirks=512)
+    with pytest.raises(pkg.native.NativeError, match="requires NFSP_EXT_LINEAR_Q"):
+        pkg.engine.SelfPlayEngine(n_lanes=64, quirks=pkg.native.EXT_MSE_Q)
+    eng = pkg.engine.SelfPlayEngine(n_lanes=64, quirks=pkg.native.QUIRKS_REFERENCE | pkg.native.TEXTBOOK_MSE)
     eng.step()
     assert eng.stats()["hands"] == 64

@@ -66,7 +66,9 @@ def _snapshot(eng):
                                          # without sampled AR actions, 112 = also without the
                                          # one-hot SL targets)
                                          ("leduc", 120), ("leduc", 112), ("tiny_memories", 120),
-                                         ("kuhn", 120), ("kuhn", 248)])
+                                         ("kuhn", 120), ("kuhn", 248),
+                                         # + NFSP_EXT_MSE_Q (504 = NFSP_TEXTBOOK_MSE)
+                                         ("leduc", 504), ("kuhn", 504)])
 def test_learner_step_matches_oracle(pkg, case, quirks):
     cfg_e, game = CASES[case]
     g = pkg.native.GAME_KUHN if game == "kuhn" else pkg.native.GAME_LEDUC

@@ -31,7 +31,7 @@ int group_rollout_launch(nfsp_engine* const*, int, const void*) { return NFSP_EI
 }
 }
 namespace nfsp { namespace chain {
-int launch_chain_br_linear(const ChainArgs&, int, bool, hipStream_t) { return NFSP_EINVAL; }
+int launch_chain_br_linear(const ChainArgs&, int, bool, bool, hipStream_t) { return NFSP_EINVAL; }
 } }
 extern "C" int nfsp_engine_destroy(nfsp_engine*) { return NFSP_OK; }
 extern "C" int nfsp_engine_get_timings(nfsp_engine*, double*, int64_t*) { return NFSP_OK; }
