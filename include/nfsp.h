@@ -359,9 +359,16 @@ int nfsp_group_rounds(nfsp_group* g, int64_t* out);   /* BR rounds of the last l
  * argmax the env executes (leduc/newenv.py:135-145).  out[0] / out[1]: best-response value
  * of seat 0 / 1 against the other seat's policy, over both dealers and all deals;
  * out[2] = out[0] + out[1] (exploitability, chips); out[3] = seat 0's on-policy value.
- * Synchronises the ctx stream. */
+ * The whole evaluation runs on the device (csrc/exploit.hip k_exploit_walk: the policies,
+ * reach top-down and best-response values bottom-up over the public tree, in f64); only
+ * the 4 results come back.  Synchronises the ctx stream. */
 int nfsp_exploitability(nfsp_ctx* ctx, const float* dev_w_ar0, const float* dev_w_ar1, int mode,
                         double* out /*[4]*/);
+/* The same for n pairs of nets at once (one workgroup per pair; e.g. every replica of an
+ * engine group): dev_w_ar0[k] / dev_w_ar1[k] are host arrays of device pointers, out[4k..4k+3]
+ * pair k's results as above. */
+int nfsp_exploitability_batch(nfsp_ctx* ctx, const float* const* dev_w_ar0, const float* const* dev_w_ar1,
+                              int n, int mode, double* out /*[4n]*/);
 
 #ifdef __cplusplus
 }

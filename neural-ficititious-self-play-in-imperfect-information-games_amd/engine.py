@@ -270,6 +270,13 @@ class EngineGroup:
     def exploitability(self, mode: int = 0, replica: int = 0) -> dict:
         return self.replicas[replica].exploitability(mode)
 
+    def exploitability_all(self, mode: int = 0) -> list:
+        """Exact exploitability of every replica's AR pair in one launch
+        (nfsp_exploitability_batch, one workgroup per replica)."""
+        w0 = [e._wptr(0, NET_AR) for e in self.replicas]
+        w1 = [e._wptr(1, NET_AR) for e in self.replicas]
+        return exploitability_batch(self.ctx, w0, w1, mode)
+
     def close(self):
         if getattr(self, "h", None):
             for e in self.replicas:
@@ -289,6 +296,18 @@ def exploitability(ctx, dev_w_ar0: int, dev_w_ar1: int, mode: int = 0) -> dict:
     out = (C.c_double * 4)()
     native.check(ctx.L.nfsp_exploitability(ctx.h, dev_w_ar0, dev_w_ar1, mode, out), "nfsp_exploitability")
     return {"br0": out[0], "br1": out[1], "exploitability": out[2], "value0": out[3]}
+
+
+def exploitability_batch(ctx, dev_w_ar0: list, dev_w_ar1: list, mode: int = 0) -> list:
+    """nfsp_exploitability_batch on n pairs of packed AR nets (lists of device pointers)."""
+    n = len(dev_w_ar0)
+    assert len(dev_w_ar1) == n
+    a0 = (C.c_void_p * max(n, 1))(*dev_w_ar0)
+    a1 = (C.c_void_p * max(n, 1))(*dev_w_ar1)
+    out = (C.c_double * (4 * max(n, 1)))()
+    native.check(ctx.L.nfsp_exploitability_batch(ctx.h, a0, a1, n, mode, out), "nfsp_exploitability_batch")
+    return [{"br0": out[4 * k], "br1": out[4 * k + 1], "exploitability": out[4 * k + 2], "value0": out[4 * k + 3]}
+            for k in range(n)]
 
 
 def _wrap_device(addr, numel, dtype, device, owner=None) -> torch.Tensor:

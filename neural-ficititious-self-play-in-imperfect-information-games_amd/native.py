@@ -103,6 +103,7 @@ SIGNATURES = {
     "nfsp_engine_last_update": (I32, [P, I32, I32, PP, PP]),
     "nfsp_engine_lane_counts": (I32, [P, PP]),
     "nfsp_exploitability": (I32, [P, P, P, I32, P]),
+    "nfsp_exploitability_batch": (I32, [P, P, P, I32, I32, P]),
     "nfsp_engine_set_loss_log": (I32, [P, I32]),
     "nfsp_engine_losses": (I32, [P, P]),
     "nfsp_engine_set_timing": (I32, [P, I32]),
