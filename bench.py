@@ -70,7 +70,7 @@ CONFIGS = {
                         label=f"C3 as {R} learner replicas x {1_048_576 // R:,} Leduc lanes on one GPU, "
                               f"each with device M_RL 200k + M_SL 2M, target sync 150, reference cadence; "
                               f"AR nets averaged over the replicas every step")
-       for R in (2, 4, 8, 16, 32, 64)},
+       for R in (2, 4, 8, 16, 32, 64, 128, 256)},
     "c5": dict(n_lanes=1_048_576, rl_capacity=200_000, sl_capacity=2_000_000, game="kuhn",
                label="C5: Kuhn swap-in, 1,048,576 lanes/GPU, C3's memories and cadence"),
     # C5's exploitability -> 0 check runs textbook NFSP with the MSE Q loss
@@ -274,6 +274,9 @@ def measure_group(pkg, name: str, steps: int, warmup: int) -> dict:
            "ms_per_step": el / steps * 1e3, "rl_inserts_per_s": rl / el,
            "rl_inserts_per_hand": rl / hands,
            "exploitability_exact_softmax": g.exploitability(0)["exploitability"],
+           # every replica's AR pair in one launch (nfsp_exploitability_batch)
+           "exploitability_exact_softmax_replica_mean": float(sum(
+               r["exploitability"] for r in g.exploitability_all(0)) / R),
            "hands_trained": int(s1["hands"])}
     g.close()
     del g
@@ -297,7 +300,7 @@ def main():
                     help="all-reduce of the AR (average-policy) gradient steps once per engine "
                          "step over the ranks (C4; shards.AvgPolicyAllReduce); auto = on for N > 1")
     ap.add_argument("--stub-step-ms", type=float, default=None, help=argparse.SUPPRESS)
-    ap.add_argument("--groups", default="c3_r4,c3_r16,c3_r64",
+    ap.add_argument("--groups", default="c3_r4,c3_r16,c3_r64,c3_r256",
                     help="engine-group configs measured beside the C3 headline at N = 1 "
                          "(`groups` in the JSON line; '' = none)")
     args = ap.parse_args()

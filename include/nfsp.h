@@ -334,7 +334,7 @@ int nfsp_engine_set_update_limit(nfsp_engine* e, int64_t max_updates);
  * A replica's handle (nfsp_group_engine) serves weights, stats, memories, the loss log and
  * timing; nfsp_engine_update / nfsp_engine_step on it are refused. */
 typedef struct nfsp_group nfsp_group;
-#define NFSP_GROUP_MAX_REPLICAS 64
+#define NFSP_GROUP_MAX_REPLICAS 256
 #define NFSP_GROUP_AVG_AR 1u
 int nfsp_group_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, int replicas, unsigned flags,
                       nfsp_group** out);

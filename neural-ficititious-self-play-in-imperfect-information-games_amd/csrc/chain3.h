@@ -31,6 +31,8 @@ struct ChainArgs {
   const ChainJob* jobs;           // device table instead, when set (engine groups: 2R workgroups)
   int B, E;
   unsigned long long* stamps;     // diagnostic build only (NFSP_CHAIN_STAMPS): phase cycles
+  int lds;                        // host side: dynamic LDS per workgroup (0: CHAIN_LDS, a CU
+                                  // to itself; engine groups of > 64 replicas share CUs)
 };
 
 // In-kernel phase stamps (cdna_hip_programming.md §7): a separate diagnostic build only.
@@ -129,6 +131,13 @@ static_assert(REC_CHUNKS % 4 == 0 && REC_QUARTER > 64 && REC_QUARTER <= 128, "re
 // itself -- no prep / target kernel's waves share its SIMDs.
 constexpr int CHAIN_LDS = 150 * 1024;
 static_assert(sizeof(Chain3Smem) <= CHAIN_LDS, "chain LDS");
+// LDS per chain workgroup when `per_cu` of them must be resident on a CU at once (engine
+// groups with more chain workgroups than CUs): an equal share of the CU's 160 KB
+inline int chain_lds_shared(int per_cu) {
+  if (per_cu <= 1) return CHAIN_LDS;
+  const int share = (160 * 1024 / per_cu) & ~1023;
+  return share - 1024 >= (int)sizeof(Chain3Smem) ? share - 1024 : (int)sizeof(Chain3Smem);
+}
 
 // exact three-term bf16 split of 8 f32 values, a pair at a time: one packed conversion
 // per pair and level (v_cvt_pk_bf16_f32, round to nearest even), the two f32 values of the
@@ -510,19 +519,22 @@ inline int set_chain_lds(std::atomic<uint64_t>& mask, const void* f0, const void
   return NFSP_OK;
 }
 
-// Launch k_chain3<RELU, loss_log, C.jobs != null> on `s` with `blocks` workgroups (after
-// setting the LDS attribute of the four instantiations once per device).
+// Launch k_chain3<RELU, loss_log, C.jobs != null> on `s` with `blocks` workgroups of C.lds
+// (else CHAIN_LDS) bytes of LDS, after setting the LDS attribute of the four instantiations
+// once per device.
 template <int RELU>
 int launch_chain(const ChainArgs& C, int blocks, bool loss_log, hipStream_t s, std::atomic<uint64_t>& attr) {
   const int rc = set_chain_lds(attr, (const void*)k_chain3<RELU, 0, 0>, (const void*)k_chain3<RELU, 1, 0>,
                                (const void*)k_chain3<RELU, 0, 1>, (const void*)k_chain3<RELU, 1, 1>);
   if (rc != NFSP_OK) return rc;
+  const int lds = C.lds > 0 ? C.lds : CHAIN_LDS;
+  if (lds < (int)sizeof(Chain3Smem) || lds > CHAIN_LDS) return nfsp::fail(NFSP_EINVAL, "chain LDS size");
   if (C.jobs) {
-    if (loss_log) k_chain3<RELU, 1, 1><<<blocks, 256, CHAIN_LDS, s>>>(C);
-    else k_chain3<RELU, 0, 1><<<blocks, 256, CHAIN_LDS, s>>>(C);
+    if (loss_log) k_chain3<RELU, 1, 1><<<blocks, 256, lds, s>>>(C);
+    else k_chain3<RELU, 0, 1><<<blocks, 256, lds, s>>>(C);
   } else {
-    if (loss_log) k_chain3<RELU, 1, 0><<<blocks, 256, CHAIN_LDS, s>>>(C);
-    else k_chain3<RELU, 0, 0><<<blocks, 256, CHAIN_LDS, s>>>(C);
+    if (loss_log) k_chain3<RELU, 1, 0><<<blocks, 256, lds, s>>>(C);
+    else k_chain3<RELU, 0, 0><<<blocks, 256, lds, s>>>(C);
   }
   NFSP_LAUNCHED("k_chain3");
   return NFSP_OK;

@@ -750,6 +750,7 @@ struct nfsp_group {
   float* w0 = nullptr;           // [2][NP] the AR nets after the last exchange
   bool w0_valid = false;
   int64_t rounds = 0;            // BR rounds of the last learner call (stats)
+  int chain_lds = 0;             // LDS per chain workgroup: 4R chains on the device's CUs
 };
 
 namespace {
@@ -782,13 +783,21 @@ extern "C" int nfsp_group_destroy(nfsp_group* g) {
 extern "C" int nfsp_group_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, int replicas, unsigned flags,
                                  nfsp_group** out) {
   NFSP_REQUIRE(ctx && cfg && out, "null argument");
-  NFSP_REQUIRE(replicas >= 1 && replicas <= NFSP_GROUP_MAX_REPLICAS, "replicas must be in [1, 64]");
+  NFSP_REQUIRE(replicas >= 1 && replicas <= NFSP_GROUP_MAX_REPLICAS, "replicas must be in [1, 256]");
   NFSP_REQUIRE((flags & ~NFSP_GROUP_AVG_AR) == 0, "unknown group flags");
   *out = nullptr;
   nfsp_group* g = new nfsp_group();
   g->ctx = ctx;
   g->R = replicas;
   g->flags = flags;
+  {
+    // up to 4R chain workgroups run at once (2R AR + a BR round's 2R): past one per CU
+    // they share CUs, each with an equal share of the LDS
+    int dev = 0, cus = 0;
+    NFSP_HIP(hipGetDevice(&dev));
+    NFSP_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    g->chain_lds = chain_lds_shared((4 * replicas + cus - 1) / (cus > 0 ? cus : 1));
+  }
   for (int r = 0; r < replicas; ++r) {
     nfsp_engine_cfg c = *cfg;
     c.seed = cfg->seed + (uint64_t)r;
@@ -978,6 +987,7 @@ static int group_update(nfsp_group* g) {
     C.jobs = d_ar;
     C.B = cfg.batch;
     C.E = cfg.epochs;
+    C.lds = g->chain_lds;
     KTimer kc(e0, KT_CHAIN_AR, g->s_ar);
     if ((rc = launch_chain_ar(C, (int)ar_jobs.size(), loss_log, g->s_ar)) != NFSP_OK) return rc;
   }
@@ -994,6 +1004,7 @@ static int group_update(nfsp_group* g) {
     C.jobs = d_br + round_off[k];
     C.B = cfg.batch;
     C.E = cfg.epochs;
+    C.lds = g->chain_lds;
     KTimer kc(e0, KT_CHAIN_BR, g->s_br);
     if ((rc = launch_br_chain(C, nj, cfg.quirks, loss_log, g->s_br)) != NFSP_OK) return rc;
   }

@@ -120,7 +120,7 @@ SIGNATURES = {
 }
 GROUP_AVG_AR = 1
 DEAL_PHILOX, DEAL_PY3_MT, DEAL_PY2_MT = 0, 1, 2
-GROUP_MAX_REPLICAS = 64
+GROUP_MAX_REPLICAS = 256
 
 _LIB = None
 
