@@ -48,7 +48,10 @@ int main(int argc, char** argv) {
   const int U = argc > 1 ? atoi(argv[1]) : 200;
   const int relu = argc > 2 ? atoi(argv[2]) : 1;
   const bool compare = argc > 3 && !strcmp(argv[3], "compare");
-  const int nblk = argc > 4 ? atoi(argv[4]) : 1;     // concurrent chains (as the AR launch: 2)
+  const int nblk = argc > 4 ? atoi(argv[4]) : 1;     // concurrent chains (as the AR launch: 2;
+                                                      // > 2: the engine-group instantiation)
+  const bool distinct = getenv("DISTINCT_RECS") && atoi(getenv("DISTINCT_RECS"));  // > 2 chains:
+                                                      // each its own copy of the records (HBM)
   const float wscale = argc > 5 ? (float)atof(argv[5]) : 1.f;   // e.g. 60: saturated softmax,
                                                                 // exercises the CE clip
   const int B = 128, E = 2, NMB = B / 32;
@@ -104,8 +107,32 @@ int main(int argc, char** argv) {
   R.lr_fixed = 0.1f; R.lr0 = 0.05;
   CK(hipFuncSetAttribute((const void*)k_chain3<0, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, CHAIN_LDS));
   CK(hipFuncSetAttribute((const void*)k_chain3<1, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, CHAIN_LDS));
+  // engine-group form: a device job table, one workgroup per chain, own weights each
+  ChainJob* djobs = nullptr;
+  if (nblk > 2) {
+    std::vector<ChainJob> jobs(nblk, C.job[0]);
+    float* wall; StepRec* rall = drec;
+    CK(hipMalloc(&wall, (size_t)nblk * w.size() * 4));
+    if (distinct) CK(hipMalloc(&rall, (size_t)nblk * rec.size() * sizeof(StepRec)));
+    for (int k = 0; k < nblk; ++k) {
+      CK(hipMemcpy(wall + (size_t)k * w.size(), w.data(), w.size() * 4, hipMemcpyHostToDevice));
+      if (distinct) CK(hipMemcpy(rall + (size_t)k * rec.size(), rec.data(), rec.size() * sizeof(StepRec), hipMemcpyHostToDevice));
+      jobs[k].w = wall + (size_t)k * w.size();
+      jobs[k].rec = rall + (distinct ? (size_t)k * rec.size() : 0);
+    }
+    CK(hipMalloc(&djobs, sizeof(ChainJob) * nblk));
+    CK(hipMemcpy(djobs, jobs.data(), sizeof(ChainJob) * nblk, hipMemcpyHostToDevice));
+    CK(hipFuncSetAttribute((const void*)k_chain3<0, 0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, CHAIN_LDS));
+    CK(hipFuncSetAttribute((const void*)k_chain3<1, 0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, CHAIN_LDS));
+  }
+  const int lds = getenv("CHAIN_LDS_BYTES") ? atoi(getenv("CHAIN_LDS_BYTES")) : CHAIN_LDS;
+  ChainArgs CT = C;
+  CT.jobs = djobs;
   auto launch3 = [&]() {
-    if (relu) k_chain3<1, 0><<<nblk, 256, CHAIN_LDS>>>(C);
+    if (nblk > 2) {
+      if (relu) k_chain3<1, 0, 1><<<nblk, 256, lds>>>(CT);
+      else k_chain3<0, 0, 1><<<nblk, 256, lds>>>(CT);
+    } else if (relu) k_chain3<1, 0><<<nblk, 256, CHAIN_LDS>>>(C);
     else k_chain3<0, 0><<<nblk, 256, CHAIN_LDS>>>(C);
   };
   if (compare) {
