@@ -430,6 +430,9 @@ __global__ void __launch_bounds__(256) k_group_avg_ar(float* const* __restrict__
   } else {
     const float base = w0[i];
     float s = 0.f;
+    // the sum stays in replica order; the unroll lets 16 replicas' loads go out together
+    // (one at a time, R = 256 took 0.2 ms of latency per step)
+#pragma unroll 16
     for (int r = 0; r < R; ++r) s = s + (war[2 * r + a][q] - base);
     nw = base + s * (1.0f / (float)R);
   }
