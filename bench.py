@@ -414,9 +414,14 @@ def main():
         with open(path) as f:
             issue = json.load(f)[net]["issue_cycles_per_step"]
         measured = k_ms[name] * 1e-3 / steps * CHAIN_CLOCK_HZ
-        return {"kernel": name, "bound": "issue", "achieved": issue, "peak": measured,
-                "unit": "cycles per SGD step (static issue / measured)", "frac": issue / measured,
-                "us_per_step": k_ms[name] * 1e3 / steps, "source": "profiles/r01_chain_census.json"}
+        out = {"kernel": name, "bound": "issue", "achieved": issue, "peak": measured,
+               "unit": "cycles per SGD step (static issue / measured)", "frac": issue / measured,
+               "us_per_step": k_ms[name] * 1e3 / steps, "source": "profiles/r01_chain_census.json"}
+        pmc = os.path.join(REPO, "profiles", "r02_chain_pmc.json")   # tools/chain_pmc.sh
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                out["sq_active_inst_frac"] = json.load(f)[net]["frac_active_inst"]
+        return out
     # the issue framing is per chain workgroup: the AR launch lasts as long as its longest
     # chain, a BR launch runs up to 2R segments side by side
     reps1, reps2 = s1.get("replicas", [s1]), s2.get("replicas", [s2])
