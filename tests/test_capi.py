@@ -52,6 +52,9 @@ def test_errors_without_gpu_are_loud(pkg):
     assert L.nfsp_create(None, 1, 0, 0, 0) == pkg.native.EINVAL
     assert b"null" in L.nfsp_last_error()
     assert L.nfsp_env_reset(None, None) == pkg.native.EINVAL
+    assert L.nfsp_exploitability(None, None, None, 0, None) == pkg.native.EINVAL
+    assert L.nfsp_exploitability_batch(None, None, None, 1, 0, None) == pkg.native.EINVAL
+    assert L.nfsp_group_create(None, None, 1, 0, None) == pkg.native.EINVAL
 
 
 def test_hand_struct_layout_matches_device_header(pkg):

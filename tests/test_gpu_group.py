@@ -115,3 +115,32 @@ def test_group_replica_refuses_its_own_update(pkg):
         g.replicas[0].step()
     g.step()                                       # the group still steps
     assert g.stats()["hands"] == 2 * SMALL["n_lanes"]
+
+
+@pytest.mark.parametrize("R", [80, 200])
+def test_group_sharing_cus_matches_standalone_engines(pkg, R):
+    """Past 64 replicas, 2 (R = 80) or 4 (R = 200) chain workgroups share a CU, each with a
+    share of its LDS (chain_lds_shared).  The chain's results must not change: replicas at
+    both ends of the group stay bit-identical to standalone engines over 2 steps."""
+    kw = dict(n_lanes=256, rl_capacity=1500, sl_capacity=1000, target_every=7)
+    g = pkg.engine.EngineGroup(R, seed=4242, init_seed=3, **kw)
+    picks = (0, R // 2, R - 1)
+    solo = {r: pkg.engine.SelfPlayEngine(seed=4242 + r, init_seed=3 + r, **kw) for r in picks}
+    for step in range(2):
+        g.step()
+        for e in solo.values():
+            e.step()
+        torch.cuda.synchronize()
+        for r in picks:
+            assert g.replicas[r].stats()["br_updates"] == solo[r].stats()["br_updates"], (step, r)
+            for x, y in zip(nets(g.replicas[r]), nets(solo[r])):
+                assert np.array_equal(x, y), (step, r)
+    assert sum(g.stats()["br_updates"]) > 0
+    g.close()
+
+
+def test_group_replica_count_bounds(pkg):
+    with pytest.raises(pkg.native.NativeError, match="replicas"):
+        pkg.engine.EngineGroup(0, **SMALL)
+    with pytest.raises(pkg.native.NativeError, match="replicas"):
+        pkg.engine.EngineGroup(pkg.native.GROUP_MAX_REPLICAS + 1, **SMALL)
