@@ -57,15 +57,11 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& A, int bx) {
   __shared__ unsigned s_act[2][3];
   __shared__ int s_rew[2];
   const int tid = threadIdx.x;
-  // stage AR0, BR0, AR1, BR1 (padded W1 rows)
+  // stage AR0, BR0, AR1, BR1 (fwd_lds layout: padded W1 rows, {b1, W2} per hidden unit)
   for (int e = tid; e < 4 * nn::NP; e += blockDim.x) {
     const int net = e / nn::NP, q = e - net * nn::NP;
     const int agent = net >> 1, kind = net & 1;
-    const float v = A.w[(agent * 3 + kind) * nn::NP + q];
-    int d;
-    if (q < nn::OB1) d = (q / nn::H) * W1S + (q % nn::H);
-    else d = LB1 + (q - nn::OB1);
-    sw[net * NET_LDS + d] = v;
+    sw[net * NET_LDS + net_lds_index(q)] = A.w[(agent * 3 + kind) * nn::NP + q];
   }
   for (int e = tid; e < 4 * nn::H; e += blockDim.x) sw[(e / nn::H) * NET_LDS + ZROW + e % nn::H] = 0.f;
   if (tid < 6) s_act[tid / 3][tid % 3] = 0;

@@ -12,11 +12,28 @@ namespace nfsp {
 namespace eng {
 
 constexpr int MAXREC = 6;          // records of one kind per lane per hand (<= 6 decisions)
-constexpr int W1S = 65;            // padded LDS row stride of W1 for per-lane row gathers:
-                                   // rows i, i' of two lanes hit banks (i + j), (i' + j) mod 32
-constexpr int LB1 = OBS * W1S, LW2 = LB1 + nn::H, LB2 = LW2 + nn::H * NA;
-constexpr int ZROW = LB2 + NA;     // a row of +0.0: fwd_lds' unused gather slots point here
-constexpr int NET_LDS = ZROW + nn::H;                          // 2,273 floats
+// A net in LDS for fwd_lds (one observation per lane): W1 rows padded to W1S = 66 floats,
+// so the per-lane row gathers read 2 hidden units at a time (ds_read_b64, 8-byte aligned)
+// and rows i, i' of two lanes hit the bank pairs 2i + j, 2i' + j (mod 64): distinct for
+// i, i' < 32.  Per hidden unit j one float4 {b1[j], W2[j][0..2]} (one broadcast
+// ds_read_b128).  ZROW, the row of +0.0 that unused gather slots point at, sits on the bank
+// pair of row 31 (62 mod 64), which no observation bit uses.  NET_LDS is a multiple of 64
+// floats, so every net of the rollout's 4 keeps this bank map.
+constexpr int W1S = 66;
+constexpr int LHB = 1984;                              // OBS * W1S = 1,980, rounded up to 16 B
+constexpr int LB2 = LHB + 4 * nn::H;                   // b2[3]
+constexpr int ZROW = 2302;                             // 35 x 64 + 62
+constexpr int NET_LDS = 2368;                          // 37 x 64 floats
+static_assert(OBS * W1S <= LHB && LHB % 4 == 0 && LB2 + NA <= ZROW, "fwd_lds layout");
+static_assert(ZROW % 64 == 62 && ZROW % 2 == 0 && ZROW + nn::H <= NET_LDS && NET_LDS % 64 == 0,
+              "fwd_lds zero row / net stride");
+// packed weight index (W1[30][H] | b1[H] | W2[H][3] | b2[3]) -> fwd_lds' LDS index
+__host__ __device__ inline int net_lds_index(int q) {
+  if (q < nn::OB1) return (q / nn::H) * W1S + (q % nn::H);
+  if (q < nn::OW2) return LHB + 4 * (q - nn::OB1);
+  if (q < nn::OB2) return LHB + 4 * ((q - nn::OW2) / NA) + 1 + (q - nn::OW2) % NA;
+  return LB2 + (q - nn::OB2);
+}
 constexpr int MAX_BATCH = 128;     // learner minibatch (config MiniBatchSize)
 constexpr int CHAIN_MB = 32;       // fit minibatch of the SGD chains (Keras batch_size)
 
@@ -134,10 +151,7 @@ enum {
 
 // Stage packed weights (W1[30][64] | b1 | W2 | b2) into the padded LDS layout of fwd_lds.
 __device__ inline void stage_net_lds(float* sw, const float* __restrict__ w, int tid, int nt) {
-  for (int q = tid; q < nn::NP; q += nt) {
-    const int d = q < nn::OB1 ? (q / nn::H) * W1S + (q % nn::H) : LB1 + (q - nn::OB1);
-    sw[d] = w[q];
-  }
+  for (int q = tid; q < nn::NP; q += nt) sw[net_lds_index(q)] = w[q];
   for (int j = tid; j < nn::H; j += nt) sw[ZROW + j] = 0.f;
 }
 
@@ -160,26 +174,39 @@ __device__ inline void fwd_lds(const float* __restrict__ sw, uint32_t x, int act
     b &= b - 1;
   }
   float o0 = 0.f, o1 = 0.f, o2 = 0.f;
-  // unrolled: the LDS reads of several hidden units go out together (the o sums keep their
-  // j order, so the result is unchanged)
-#pragma unroll 8
-  for (int j = 0; j < nn::H; ++j) {
-    float acc = 0.f;
+  // two hidden units per iteration (one 8-byte gather per set bit), unrolled so the LDS
+  // reads of several units go out together; every sum keeps its order (bits ascending per
+  // unit, units ascending into o), so the result is unchanged
+#pragma unroll 4
+  for (int j = 0; j < nn::H; j += 2) {
+    float a0 = 0.f, a1 = 0.f;
 #pragma unroll
-    for (int u = 0; u < 9; ++u) acc = acc + sw[rows[u] + j];
+    for (int u = 0; u < 9; ++u) {
+      const float2 v = *reinterpret_cast<const float2*>(sw + rows[u] + j);
+      a0 = a0 + v.x;
+      a1 = a1 + v.y;
+    }
     if (b) {   // > 9 set bits: impossible for Leduc observations, kept exact anyway
       uint32_t rest = b;
       while (rest) {
         const int i = __builtin_ctz(rest);
         rest &= rest - 1;
-        acc = acc + sw[i * W1S + j];
+        a0 = a0 + sw[i * W1S + j];
+        a1 = a1 + sw[i * W1S + j + 1];
       }
     }
-    float h = acc + sw[LB1 + j];
+    const float4 p0 = *reinterpret_cast<const float4*>(sw + LHB + 4 * j);
+    const float4 p1 = *reinterpret_cast<const float4*>(sw + LHB + 4 * j + 4);
+    float h = a0 + p0.x;
     h = h > 0.f ? h : 0.f;
-    o0 = o0 + h * sw[LW2 + 3 * j + 0];
-    o1 = o1 + h * sw[LW2 + 3 * j + 1];
-    o2 = o2 + h * sw[LW2 + 3 * j + 2];
+    o0 = o0 + h * p0.y;
+    o1 = o1 + h * p0.z;
+    o2 = o2 + h * p0.w;
+    h = a1 + p1.x;
+    h = h > 0.f ? h : 0.f;
+    o0 = o0 + h * p1.y;
+    o1 = o1 + h * p1.z;
+    o2 = o2 + h * p1.w;
   }
   o0 = o0 + sw[LB2 + 0];
   o1 = o1 + sw[LB2 + 1];
