@@ -236,6 +236,26 @@ def check_world(args, world: int):
             sys.exit(2)
 
 
+_RESULT_OUT = None
+
+
+def claim_stdout():
+    """In a rank process: keep the real stdout for the one JSON result line and send
+    everything else written to fd 1 -- Python prints and native libraries' chatter (gloo's
+    peer-connection lines, RCCL / HIP banners) -- to stderr."""
+    global _RESULT_OUT
+    if _RESULT_OUT is None:
+        sys.stdout.flush()
+        _RESULT_OUT = os.fdopen(os.dup(1), "w")
+        os.dup2(2, 1)
+
+
+def emit_result(obj: dict):
+    out = _RESULT_OUT if _RESULT_OUT is not None else sys.stdout
+    out.write(json.dumps(obj) + "\n")
+    out.flush()
+
+
 def stub_main(args, world, rank, dist):
     """Test hook (`--stub-step-ms`): the launcher and the timing protocol with a CPU sleep in
     place of the engine step (no GPU).  Never a measurement: `data` says "stub"."""
@@ -243,11 +263,11 @@ def stub_main(args, world, rank, dist):
     elapsed = timed_steps(lambda: time.sleep(args.stub_step_ms * 1e-3 * (1 + 0.5 * rank)),
                           args.steps, args.warmup, dist, device="cpu")
     if rank == 0:
-        print(json.dumps({"metric": "Leduc self-play hands/sec", "unit": "hands/s",
-                          "value": job_value(args.steps * lanes, world, elapsed), "n_gpus": world,
-                          "steps": args.steps, "warmup": args.warmup,
-                          "ms_per_step": elapsed / args.steps * 1e3, "data": "stub",
-                          "config": {"parallelism": f"dp{world}"}}), flush=True)
+        emit_result({"metric": "Leduc self-play hands/sec", "unit": "hands/s",
+                     "value": job_value(args.steps * lanes, world, elapsed), "n_gpus": world,
+                     "steps": args.steps, "warmup": args.warmup,
+                     "ms_per_step": elapsed / args.steps * 1e3, "data": "stub",
+                     "config": {"parallelism": f"dp{world}"}})
     if dist is not None:
         dist.destroy_process_group()
 
@@ -308,6 +328,7 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # the driver's `bench.py --gpus N` without torch.distributed.run: one rank per GPU
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    claim_stdout()
     check_world(args, int(os.environ.get("WORLD_SIZE", "1")))
     if args.stub_step_ms is not None:
         world, rank, _, dist = init_dist("gloo")
@@ -499,7 +520,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, threads, cfg)
         out["cpu_baseline_numpy"] = cpu_baseline_numpy(min(args.cpu_seconds, 5.0), cfg.get("game", "leduc"))
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit_result(out)
     if dist is not None:
         dist.destroy_process_group()
 

@@ -2,9 +2,11 @@
 and device sync around exactly K timed steps, the MAX elapsed over ranks, and the whole-job
 value = units of all ranks / that time (bench.py timed_steps / job_value).  The GPU engine
 itself is replaced by a CPU step of known, rank-dependent duration."""
+import json
 import multiprocessing as mp
 import os
 import socket
+import subprocess
 import sys
 import time
 
@@ -53,6 +55,12 @@ def test_gpus_flag_launches_the_ranks():
                              "--config", "c2"])
     assert rc == 0, err
     assert len(lines) == 1, lines
+    # stdout holds the result line only: the ranks send every other write to fd 1 (gloo's
+    # "Rank k is connected" lines, library banners) to stderr
+    stdout = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "1",
+                             "--warmup", "0", "--stub-step-ms", "1"], capture_output=True, text=True,
+                            timeout=120, env={k: v for k, v in os.environ.items() if k != "WORLD_SIZE"}).stdout
+    assert len(stdout.splitlines()) == 1 and json.loads(stdout)["n_gpus"] == 2, stdout
     out = lines[0]
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2"
     # rank 1 sleeps 1.5x as long: the job time is the slow rank's
