@@ -10,7 +10,7 @@ vector issue for 8 of its 16 cycles), s_nop 4; LDS / VMEM / SALU / waitcnt / bra
 bench.py divides that issue estimate by the measured cycles per step: the fraction of a
 step one wave spends issuing (the chain is one wave per SIMD, so nothing else fills it).
 
-    python tools/chain_census.py > profiles/r01_chain_census.json
+    python tools/chain_census.py > profiles/r02_chain_census.json
 """
 import collections
 import json
@@ -57,6 +57,8 @@ def price(op):
         return "mfma", 8
     if op.startswith(TRANS):
         return "trans", 8
+    if op.startswith("v_dot2"):        # two passes (MI355X_MICROARCH: ~10 beside MFMAs)
+        return "dot2", 8
     if op.startswith("v_"):
         return "valu", 4
     if op == "s_nop":
@@ -70,8 +72,8 @@ def price(op):
 
 def main():
     out = {"source": "tools/chain_census.py (gfx950 assembly with the build's flags)",
-           "prices": "MI355X_MICROARCH.md issue costs: VALU 4, transcendental 8, MFMA 16x16x32 8, "
-                     "s_nop 4, other 1 cycle"}
+           "prices": "MI355X_MICROARCH.md issue costs: VALU 4, transcendental 8, v_dot2 8, "
+                     "MFMA 16x16x32 8, s_nop 4, other 1 cycle"}
     for name, (src, kern) in KERNELS.items():
         body = loop_body(asm(src), kern)
         ops = collections.Counter(l.split()[0] for l in body)
