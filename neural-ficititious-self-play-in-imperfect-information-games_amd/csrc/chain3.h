@@ -148,9 +148,11 @@ inline int chain_lds_shared(int per_cu) {
 // (tools/chain_ab.sh).  Two details:
 //  * the (-1, 0) / (0, -1) operands come from VGPRs: written as the literal 0x0000bf80 the
 //    pair did not reach the instruction as given;
-//  * the conversions are plain C++ casts, so the compiler sees every producer and consumer
-//    of the dot2c results; with the conversion as inline asm the chain's results moved
-//    (up to 2e-3 after 200 updates), although each residual alone was exact
+//  * the conversions are plain C++ casts, so the compiler sees every consumer of the dot2c
+//    results: gfx950 needs wait states between a DOT instruction's write and another VALU
+//    instruction's read, which the compiler inserts only for instructions it knows.  With
+//    the conversion as inline asm the chain's results moved (up to 2e-3 after 200 updates),
+//    although each residual alone was exact
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 __device__ inline uint32_t cvt_pk_bf16(float a, float b) {
   const bf16x2 r = {(__bf16)a, (__bf16)b};
