@@ -16,8 +16,8 @@ from collections import defaultdict
 
 # bench.py kernel label -> substring of the rocprof kernel name
 KERNELS = {
-    "k_chain3_br": "k_chain3<1, 0>",
-    "k_chain3_ar": "k_chain3<0, 0>",
+    "k_chain3_br": "k_chain3<1, 0, 0>",     # the one-engine instantiations (TABLE = 0)
+    "k_chain3_ar": "k_chain3<0, 0, 0>",
     "k_rollout": "k_rollout(",
     "k_commit": "k_commit(",
     "k_br_targets": "k_br_targets(",
