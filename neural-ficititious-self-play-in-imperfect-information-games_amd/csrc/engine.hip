@@ -142,24 +142,29 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& A, int bx) {
       if (!t) {
         const uint32_t x = nfsp::hand_obs(h, p);
         float y[3];
-        if (!polBR[p]) {
-          fwd_lds(sw + (p * 2 + 0) * NET_LDS, x, NFSP_ACT_SOFTMAX, y);
-          if (A.quirks & NFSP_EXT_SAMPLE_AR) {   // sample the average policy (textbook NFSP)
-            const u32x4 u = nfsp::philox4x32({(uint32_t)L, A.g_lo, A.g_hi, 0x80000000u + (uint32_t)dec_ar},
-                                             A.k0, A.k1);
-            dec_ar++;
-            const float r = nfsp::u01(u.x);
-            const int v = r < y[0] ? 0 : (r < y[0] + y[1] ? 1 : 2);
-            y[0] = v == 0 ? 1.f : 0.f; y[1] = v == 1 ? 1.f : 0.f; y[2] = v == 2 ? 1.f : 0.f;
-          }
-        } else {
-          const u32x4 u = nfsp::philox4x32({(uint32_t)L, A.g_lo, A.g_hi, 2u + (uint32_t)dec}, A.k0, A.k1);
+        // one forward for the whole wave: the net (AR or BR of seat p) is a per-lane LDS
+        // base, so lanes acting with different nets share the instructions instead of the
+        // wave running an AR and a BR forward one after the other
+        const bool br = polBR[p] != 0;
+        bool fwd = true;
+        u32x4 ub{};
+        if (br) {                  // act_best_response's eps draw (agent/agent.py:124-128)
+          ub = nfsp::philox4x32({(uint32_t)L, A.g_lo, A.g_hi, 2u + (uint32_t)dec}, A.k0, A.k1);
           dec++;
-          if ((double)nfsp::u01(u.x) > (p ? eps1 : eps0)) {
-            fwd_lds(sw + (p * 2 + 1) * NET_LDS, x, br_act(A.quirks), y);
-          } else {                 // np.random.rand(1, 1, 3)
-            y[0] = nfsp::u01(u.y); y[1] = nfsp::u01(u.z); y[2] = nfsp::u01(u.w);
-          }
+          fwd = (double)nfsp::u01(ub.x) > (p ? eps1 : eps0);
+        }
+        if (fwd) {
+          fwd_lds(sw + (p * 2 + (br ? 1 : 0)) * NET_LDS, x, br ? br_act(A.quirks) : NFSP_ACT_SOFTMAX, y);
+        } else {                   // np.random.rand(1, 1, 3)
+          y[0] = nfsp::u01(ub.y); y[1] = nfsp::u01(ub.z); y[2] = nfsp::u01(ub.w);
+        }
+        if (!br && (A.quirks & NFSP_EXT_SAMPLE_AR)) {   // sample the average policy (textbook NFSP)
+          const u32x4 u = nfsp::philox4x32({(uint32_t)L, A.g_lo, A.g_hi, 0x80000000u + (uint32_t)dec_ar},
+                                           A.k0, A.k1);
+          dec_ar++;
+          const float r = nfsp::u01(u.x);
+          const int v = r < y[0] ? 0 : (r < y[0] + y[1] ? 1 : 2);
+          y[0] = v == 0 ? 1.f : 0.f; y[1] = v == 1 ? 1.f : 0.f; y[2] = v == 2 ? 1.f : 0.f;
         }
         nfsp::hand_step(h, p, y[0], y[1], y[2]);
         acted = true;
