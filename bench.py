@@ -294,9 +294,6 @@ def measure_group(pkg, name: str, steps: int, warmup: int) -> dict:
            "ms_per_step": el / steps * 1e3, "rl_inserts_per_s": rl / el,
            "rl_inserts_per_hand": rl / hands,
            "exploitability_exact_softmax": g.exploitability(0)["exploitability"],
-           # every replica's AR pair in one launch (nfsp_exploitability_batch)
-           "exploitability_exact_softmax_replica_mean": float(sum(
-               r["exploitability"] for r in g.exploitability_all(0)) / R),
            "hands_trained": int(s1["hands"])}
     g.close()
     del g

@@ -789,18 +789,16 @@ extern "C" int nfsp_group_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, int 
   NFSP_REQUIRE(replicas >= 1 && replicas <= NFSP_GROUP_MAX_REPLICAS, "replicas must be in [1, 256]");
   NFSP_REQUIRE((flags & ~NFSP_GROUP_AVG_AR) == 0, "unknown group flags");
   *out = nullptr;
+  // up to 4R chain workgroups run at once (2R AR + a BR round's 2R): past one per CU they
+  // share CUs, each with an equal share of the LDS
+  int dev = 0, cus = 0;
+  NFSP_HIP(hipGetDevice(&dev));
+  NFSP_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   nfsp_group* g = new nfsp_group();
   g->ctx = ctx;
   g->R = replicas;
   g->flags = flags;
-  {
-    // up to 4R chain workgroups run at once (2R AR + a BR round's 2R): past one per CU
-    // they share CUs, each with an equal share of the LDS
-    int dev = 0, cus = 0;
-    NFSP_HIP(hipGetDevice(&dev));
-    NFSP_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    g->chain_lds = chain_lds_shared((4 * replicas + cus - 1) / (cus > 0 ? cus : 1));
-  }
+  g->chain_lds = chain_lds_shared((4 * replicas + cus - 1) / (cus > 0 ? cus : 1));
   for (int r = 0; r < replicas; ++r) {
     nfsp_engine_cfg c = *cfg;
     c.seed = cfg->seed + (uint64_t)r;
