@@ -982,15 +982,25 @@ static int group_update(nfsp_group* g) {
       NFSP_LAUNCHED("k_res_apply");
     }
   }
-  if (!ar_jobs.empty()) {
+  // When chains share CUs (R > 64), the first round's BR targets run before the AR chains
+  // start: alone they take the chip's issue slots instead of competing with 2R resident AR
+  // chains, and the BR stream is the longer one at that size.  (No data dependency.)
+  const bool shared_cus = g->chain_lds < CHAIN_LDS;
+  auto launch_ar = [&](hipEvent_t after) -> int {
     NFSP_HIP(hipStreamWaitEvent(g->s_ar, fork, 0));
+    if (after) NFSP_HIP(hipStreamWaitEvent(g->s_ar, after, 0));
     ChainArgs C{};
     C.jobs = d_ar;
     C.B = cfg.batch;
     C.E = cfg.epochs;
     C.lds = g->chain_lds;
     KTimer kc(e0, KT_CHAIN_AR, g->s_ar);
-    if ((rc = launch_chain_ar(C, (int)ar_jobs.size(), loss_log, g->s_ar)) != NFSP_OK) return rc;
+    return launch_chain_ar(C, (int)ar_jobs.size(), loss_log, g->s_ar);
+  };
+  bool ar_launched = ar_jobs.empty();
+  if (!shared_cus && !ar_launched) {
+    if ((rc = launch_ar(nullptr)) != NFSP_OK) return rc;
+    ar_launched = true;
   }
   NFSP_HIP(hipStreamWaitEvent(g->s_br, fork_br, 0));
   for (size_t k = 0; k < rounds; ++k) {
@@ -1001,6 +1011,13 @@ static int group_update(nfsp_group* g) {
           d_tg + round_off[k], TargetJob{}, cfg.batch, cfg.epochs, cfg.gamma, cfg.quirks, cfg.lr_br);
     }
     NFSP_LAUNCHED("k_br_targets");
+    if (!ar_launched) {
+      hipEvent_t t0 = take_event(e0);
+      NFSP_HIP(hipEventRecord(t0, g->s_br));
+      if ((rc = launch_ar(t0)) != NFSP_OK) return rc;
+      e0->pool.push_back(t0);
+      ar_launched = true;
+    }
     ChainArgs C{};
     C.jobs = d_br + round_off[k];
     C.B = cfg.batch;
@@ -1009,6 +1026,7 @@ static int group_update(nfsp_group* g) {
     KTimer kc(e0, KT_CHAIN_BR, g->s_br);
     if ((rc = launch_br_chain(C, nj, cfg.quirks, loss_log, g->s_br)) != NFSP_OK) return rc;
   }
+  if (!ar_launched && (rc = launch_ar(nullptr)) != NFSP_OK) return rc;
   for (hipStream_t st : {g->s_ar, g->s_br}) {
     hipEvent_t j = take_event(e0);
     NFSP_HIP(hipEventRecord(j, st));
