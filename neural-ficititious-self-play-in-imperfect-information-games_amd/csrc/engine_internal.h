@@ -161,15 +161,16 @@ __device__ inline void stage_net_lds(float* sw, const float* __restrict__ w, int
 __host__ __device__ inline int br_act(unsigned quirks) {
   return (quirks & NFSP_EXT_LINEAR_Q) ? NFSP_ACT_LINEAR : NFSP_ACT_RELU;
 }
-__device__ inline void fwd_lds(const float* __restrict__ sw, uint32_t x, int act, float y[3]) {
+template <int NR>   // gather rows per hidden unit: 9 covers any Leduc observation
+__device__ inline void fwd_lds_n(const float* __restrict__ sw, uint32_t x, int act, float y[3]) {
 #pragma clang fp contract(off)
   // the set bits' W1 rows in ascending order; the unused slots point at the zero row, so
   // every hidden unit adds 9 terms without a branch.  Exact: acc starts at +0 and only
   // gains finite values, so it is never -0, and a trailing + 0.0 leaves it unchanged.
-  int rows[9];
+  int rows[NR];
   uint32_t b = x;
 #pragma unroll
-  for (int u = 0; u < 9; ++u) {
+  for (int u = 0; u < NR; ++u) {
     rows[u] = b ? __builtin_ctz(b) * W1S : ZROW;
     b &= b - 1;
   }
@@ -181,12 +182,12 @@ __device__ inline void fwd_lds(const float* __restrict__ sw, uint32_t x, int act
   for (int j = 0; j < nn::H; j += 2) {
     float a0 = 0.f, a1 = 0.f;
 #pragma unroll
-    for (int u = 0; u < 9; ++u) {
+    for (int u = 0; u < NR; ++u) {
       const float2 v = *reinterpret_cast<const float2*>(sw + rows[u] + j);
       a0 = a0 + v.x;
       a1 = a1 + v.y;
     }
-    if (b) {   // > 9 set bits: impossible for Leduc observations, kept exact anyway
+    if (NR == 9 && b) {   // > 9 set bits: impossible for Leduc observations, kept exact anyway
       uint32_t rest = b;
       while (rest) {
         const int i = __builtin_ctz(rest);
@@ -223,6 +224,14 @@ __device__ inline void fwd_lds(const float* __restrict__ sw, uint32_t x, int act
     const float s = (e0 + e1) + e2;
     y[0] = e0 / s; y[1] = e1 / s; y[2] = e2 / s;
   }
+}
+
+
+// The wave picks the 7-row body when no active lane has more than 7 set bits (one ballot):
+// the rows a lane does not have read the zero row, so both bodies give the same sums.
+__device__ inline void fwd_lds(const float* __restrict__ sw, uint32_t x, int act, float y[3]) {
+  if (__ballot(__popc(x) > 7)) fwd_lds_n<9>(sw, x, act, y);
+  else fwd_lds_n<7>(sw, x, act, y);
 }
 
 }  // namespace eng
