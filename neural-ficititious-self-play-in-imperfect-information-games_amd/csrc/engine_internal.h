@@ -227,11 +227,14 @@ __device__ inline void fwd_lds_n(const float* __restrict__ sw, uint32_t x, int a
 }
 
 
-// The wave picks the 7-row body when no active lane has more than 7 set bits (one ballot):
-// the rows a lane does not have read the zero row, so both bodies give the same sums.
+// The wave picks the 5-, 7- or 9-row body by the most set bits any active lane has (a
+// ballot or two): rows a lane does not have read the zero row, so every body gives the
+// same sums.
 __device__ inline void fwd_lds(const float* __restrict__ sw, uint32_t x, int act, float y[3]) {
-  if (__ballot(__popc(x) > 7)) fwd_lds_n<9>(sw, x, act, y);
-  else fwd_lds_n<7>(sw, x, act, y);
+  const int pc = __popc(x);
+  if (__ballot(pc > 7)) fwd_lds_n<9>(sw, x, act, y);
+  else if (__ballot(pc > 5)) fwd_lds_n<7>(sw, x, act, y);
+  else fwd_lds_n<5>(sw, x, act, y);
 }
 
 }  // namespace eng
