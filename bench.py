@@ -52,9 +52,16 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 CONFIGS = {
-    "c3": dict(n_lanes=1_048_576, rl_capacity=200_000, sl_capacity=2_000_000,
-               label="C3: 1,048,576 Leduc lanes/GPU, device M_RL 200k + M_SL 2M, target sync 150, "
-                     "reference update cadence (1 update_strategy / 128 RL inserts / agent)"),
+    # C3 advances its 1M lanes in 16 slices of 65,536, the learner consuming each slice's
+    # inserts before the next acts (include/nfsp.h cfg.slices): the policy lag is one slice,
+    # and C3 learns inside the CPU reference's seed band (tests/test_gpu_slices.py)
+    "c3": dict(n_lanes=1_048_576, slices=16, rl_capacity=200_000, sl_capacity=2_000_000,
+               label="C3: 1,048,576 Leduc lanes/GPU (advanced in 16 slices of 65,536), device M_RL 200k "
+                     "+ M_SL 2M, target sync 150, reference update cadence (1 update_strategy / 128 RL "
+                     "inserts / agent)"),
+    "c3_1slice": dict(n_lanes=1_048_576, rl_capacity=200_000, sl_capacity=2_000_000,
+                      label="C3 with all 1,048,576 lanes in one rollout per step (round 2's form: policy "
+                            "lag of 1M hands), M_RL 200k + M_SL 2M, reference cadence"),
     "c2": dict(n_lanes=65_536, rl_capacity=40_000, sl_capacity=40_000,
                label="C2: 65,536 Leduc lanes/GPU, M_RL/M_SL 40k, eta 0.1, 2x64 MLP heads, "
                      "reference update cadence"),
@@ -160,12 +167,16 @@ def init_dist(backend=None):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world == 1:
         return world, rank, local, None
+    import datetime
     import torch.distributed as dist
     backend = backend or "nccl"
+    # bounded: a rank whose peer never arrives fails in 2 minutes, not the default 10-30
+    timeout = datetime.timedelta(seconds=float(os.environ.get("NFSP_PG_TIMEOUT_S", "120")))
     if backend == "nccl":
-        dist.init_process_group(backend, device_id=torch.device("cuda", local % torch.cuda.device_count()))
+        dist.init_process_group(backend, timeout=timeout,
+                                device_id=torch.device("cuda", local % torch.cuda.device_count()))
     else:
-        dist.init_process_group(backend)
+        dist.init_process_group(backend, timeout=timeout)
     return world, rank, local, dist
 
 
@@ -205,21 +216,46 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def launch_ranks(n: int, argv: list[str]) -> int:
+def launch_ranks(n: int, argv: list[str], poll_s: float = 0.2) -> int:
     """`bench.py --gpus N` started without a torch.distributed environment: start N rank
     processes of this script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR 127.0.0.1 /
-    MASTER_PORT set, one rank per GPU), wait for all, and return the worst exit code.  The
-    parent never touches the GPU (no torch.cuda call: it only forks children), so the
-    children own the devices; rank 0 prints the JSON line."""
+    MASTER_PORT set, one rank per GPU) and wait for them.  Fail fast: the first rank to exit
+    non-zero (OOM, RCCL init, a HIP error) ends the job -- its siblings, which would otherwise
+    block in a barrier or all-reduce until the process-group timeout, are terminated (then
+    killed after 10 s) and its exit code is returned.  The parent never touches the GPU (no
+    torch.cuda call: it only forks children), so the children own the devices; rank 0 prints
+    the JSON line."""
     port = _free_port()
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
-    rcs = [p.wait() for p in procs]
-    bad = [rc for rc in rcs if rc != 0]
-    return bad[0] if bad else 0
+    failed = None
+    while failed is None and any(p.poll() is None for p in procs):
+        for r, p in enumerate(procs):
+            rc = p.poll()
+            if rc is not None and rc != 0:
+                failed = (r, rc)
+                break
+        else:
+            time.sleep(poll_s)
+    if failed is None:
+        bad = [p.returncode for p in procs if p.returncode != 0]
+        return bad[0] if bad else 0
+    r, rc = failed
+    sys.stderr.write(f"bench.py: rank {r} exited with {rc}; stopping the other ranks\n")
+    for p in procs:
+        if p.poll() is None:
+            p.terminate()
+    deadline = time.time() + 10.0
+    for p in procs:
+        try:
+            p.wait(timeout=max(0.1, deadline - time.time()))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+    return rc
 
 
 def check_world(args, world: int):
@@ -260,6 +296,11 @@ def stub_main(args, world, rank, dist):
     """Test hook (`--stub-step-ms`): the launcher and the timing protocol with a CPU sleep in
     place of the engine step (no GPU).  Never a measurement: `data` says "stub"."""
     lanes = CONFIGS[args.config]["n_lanes"]
+    if args.stub_fail:
+        fr, fc = (int(v) for v in args.stub_fail.split(":"))
+        if rank == fr:
+            sys.stderr.write(f"stub: rank {rank} fails with {fc}\n")
+            os._exit(fc)
     elapsed = timed_steps(lambda: time.sleep(args.stub_step_ms * 1e-3 * (1 + 0.5 * rank)),
                           args.steps, args.warmup, dist, device="cpu")
     if rank == 0:
@@ -317,6 +358,8 @@ def main():
                     help="all-reduce of the AR (average-policy) gradient steps once per engine "
                          "step over the ranks (C4; shards.AvgPolicyAllReduce); auto = on for N > 1")
     ap.add_argument("--stub-step-ms", type=float, default=None, help=argparse.SUPPRESS)
+    # test hook with --stub-step-ms: rank R exits with code C after the process group is up
+    ap.add_argument("--stub-fail", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--groups", default="c3_r4,c3_r16,c3_r64,c3_r256",
                     help="engine-group configs measured beside the C3 headline at N = 1 "
                          "(`groups` in the JSON line; '' = none)")
@@ -346,7 +389,7 @@ def main():
                                      sl_capacity=cfg["sl_capacity"], seed=1234 + R * rank,
                                      init_seed=R * rank, game=game, avg_ar=True)
     else:
-        extra = {"quirks": cfg["quirks"]} if "quirks" in cfg else {}
+        extra = {k: cfg[k] for k in ("quirks", "slices") if k in cfg}
         eng = pkg.engine.SelfPlayEngine(n_lanes=cfg["n_lanes"], rl_capacity=cfg["rl_capacity"],
                                         sl_capacity=cfg["sl_capacity"], seed=1234 + rank,
                                         init_seed=rank, game=game, **extra)
@@ -390,11 +433,18 @@ def main():
     t_rl, t_sl = rl_ins / hands_rank, sl_ins / hands_rank
     bytes_hand = BYTES_RL * t_rl + BYTES_SL * t_sl
     rollout_bytes = bytes_hand * cfg["n_lanes"] / R                       # per launch
+    # the rollout writes bit-packed staging records, not the reference's fp32 tuples: the
+    # tuple bytes are a reference-layout EQUIVALENT; `traffic` / `achieved_counter` are what
+    # the kernel moves (rocprofv3 PMC, profiles/pmc_<config>.json)
     roof_rollout = {"kernel": "k_rollout", "bound": "hbm",
                     "achieved": rollout_bytes / (k_ms["k_rollout"] * 1e-3) / 1e9,
-                    "peak": PEAK_HBM_GBS, "unit": "GB/s", "traffic": None,
+                    "achieved_is": "reference-layout-equivalent bytes (257 B / 132 B fp32 tuples)",
+                    "peak": PEAK_HBM_GBS, "unit": "GB/s", "traffic": load_pmc(args.config, "k_rollout"),
                     "bytes_per_hand": bytes_hand, "avg_ms": k_ms["k_rollout"]}
     roof_rollout["frac"] = roof_rollout["achieved"] / PEAK_HBM_GBS
+    if roof_rollout["traffic"]:
+        roof_rollout["achieved_counter"] = roof_rollout["traffic"] / (k_ms["k_rollout"] * 1e-3) / 1e9
+        roof_rollout["frac_counter"] = roof_rollout["achieved_counter"] / PEAK_HBM_GBS
     # SURVEY 8(d)'s whole-path figure: rollout writes + the sampled reads at the reference
     # cadence (T_rl / 128 updates x 128 rows x (257 + 132) B) per hand, over the timed step
     step_bytes_hand = bytes_hand + (t_rl / 128.0) * 128 * (BYTES_RL + BYTES_SL)
@@ -456,11 +506,17 @@ def main():
              # one AR launch runs both agents' chains side by side: it lasts as long as the
              # agent with more updates
              "k_chain3_ar_issue": chain_issue("k_chain3_ar", ar_max, "ar")}
-    # the dominant kernel = largest GPU time inside the timed region
-    singles = [k for k in timings if k not in ("learner", "learner_prep")]
-    dom = max(singles, key=lambda k: timings[k][0])
-    roof_key = f"{dom}_hbm" if f"{dom}_hbm" in roofs else "k_rollout_hbm"
+    # the dominant kernel = the one on the learner's critical path: the streams run side by
+    # side (AR chains of both agents on one stream, each agent's BR targets + chains on its
+    # own), so GPU time summed over streams overstates the BR chain; the stream whose busy
+    # span per step is longest bounds the step, and its chain is the roofline kernel
+    streams = {"ar_chain": k_step_ms["k_chain3_ar"], "br_stream_a0": k_step_ms["br_stream_a0"],
+               "br_stream_a1": k_step_ms["br_stream_a1"]}
+    crit = max(streams, key=streams.get)
+    dom = "k_chain3_ar" if crit == "ar_chain" else "k_chain3_br"
+    roof_key = f"{dom}_hbm"
     roofline = dict(roofs[roof_key])
+    roofline["critical_stream"] = crit
     pmc = load_pmc(args.config, roofline["kernel"])
     if pmc is not None:
         roofline["traffic"] = pmc
@@ -492,6 +548,8 @@ def main():
         "kernel_ms": k_ms,
         "kernel_ms_per_step": k_step_ms,
         "kernel_ms_source": "HIP events around every launch, second pass of K steps",
+        "stream_ms_per_step": streams,
+        "slices": cfg.get("slices", 1),
         "rollout_only_hands_per_s": cfg["n_lanes"] / (rollout_path_ms * 1e-3) * world,
         "per_step": {"br_updates": br_upd / args.steps, "ar_updates": ar_upd / args.steps,
                      "rl_inserts_per_hand": t_rl, "sl_inserts_per_hand": t_sl},

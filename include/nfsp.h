@@ -244,6 +244,17 @@ typedef struct nfsp_engine_cfg {
   float eta, lr_br, lr_ar;     /* 0.1, 0.05, 0.1 */
   double gamma, epsilon;       /* 0.95, 0.06 */
   uint64_t seed;
+  /* Lane slices (1 = off).  The n_lanes envs are advanced in `slices` equal slices of
+   * n_lanes / slices lanes: nfsp_rollout plays one hand on every lane of the next slice, and
+   * nfsp_engine_step = `slices` x (nfsp_rollout + nfsp_engine_update), i.e. one hand per lane
+   * of all n_lanes, with the learner consuming each slice's inserts before the next slice
+   * acts.  That bounds the declared policy lag by one slice instead of all n_lanes hands
+   * (the reference has none: main.py:27-67 learns inside the hand loop,
+   * agent/agent.py:153-154).  Philox counters and the dealer use the global lane id
+   * (slice * n_lanes / slices + lane) and the lane's hand count (rollouts / slices), so a
+   * lane's hand does not depend on the slicing.  Staging and learner buffers are sized for
+   * one slice.  n_lanes must be a multiple of slices. */
+  int32_t slices;
 } nfsp_engine_cfg;
 
 typedef struct nfsp_engine_stats {
@@ -288,10 +299,14 @@ int nfsp_engine_memories(nfsp_engine* e, int agent, nfsp_records* rl, int64_t* r
                          nfsp_records* sl, uint32_t** dev_pending_sl_obs,
                          float** dev_pending_sl_a, int64_t** dev_pending_sl_rl_pos);
 /* Per-kernel timing with HIP events recorded around each launch on the stream it runs on:
- * ms / launches [8] = {k_rollout, k_scan1+k_scan2, k_commit, learner (whole
+ * ms / launches [10] = {k_rollout, k_scan1+k_scan2, k_commit, learner (whole
  * nfsp_engine_update), learner prep (k_br_prep..k_res_apply), k_br_targets,
- * k_chain3<BR>, k_chain3<AR>}, accumulated since the previous nfsp_engine_get_timings
- * (which synchronises and resets them). */
+ * k_chain3<BR>, k_chain3<AR>, BR stream of agent 0, BR stream of agent 1}, accumulated since
+ * the previous nfsp_engine_get_timings (which synchronises and resets them).  A "BR stream"
+ * entry is the span of one learner call's BR work of that agent on its stream, from its
+ * first k_br_targets to its last chain, gaps included (engine groups: their one BR stream in
+ * slot 8) -- with k_chain3<AR> (one launch per call, both agents), the per-stream critical
+ * path of the learner. */
 int nfsp_engine_set_timing(nfsp_engine* e, int on);
 /* Loss log (observability; the reference's TensorBoard callbacks on fit, agent/agent.py:
  * 84-88,243,264): when on, the SGD chains also record each update's Keras epoch losses
@@ -301,12 +316,13 @@ int nfsp_engine_set_timing(nfsp_engine* e, int on);
  * nfsp_engine_update's updates and [.. + 1] = its last update's final-epoch loss (NaN: none). */
 int nfsp_engine_set_loss_log(nfsp_engine* e, int on);
 int nfsp_engine_losses(nfsp_engine* e, double* out /*[2][2][2]*/);
-int nfsp_engine_get_timings(nfsp_engine* e, double* ms /*[8]*/, int64_t* launches /*[8]*/);
+int nfsp_engine_get_timings(nfsp_engine* e, double* ms /*[10]*/, int64_t* launches /*[10]*/);
 /* Debug view of the last learner run: per agent and role (0 = AR, 1 = BR) the sampled
  * rows [batch] (int64) and fit permutations [epochs][batch] (int32) of its LAST update. */
 int nfsp_engine_last_update(nfsp_engine* e, int agent, int role, int64_t** dev_rows,
                             int32_t** dev_perms);
-/* Debug view of the last rollout's per-lane record counts [n_lanes] (uint32, device):
+/* Debug view of the last rollout's per-lane record counts [n_lanes / slices] (uint32, device;
+ * local lane i of the slice that rollout played is global lane slice * n_lanes / slices + i):
  * rl0 | rl1 << 4 | sl0 << 8 | sl1 << 12 (RL / SL inserts of agents 0 and 1 by that lane's
  * hand).  Their exclusive prefix over lanes is each lane's first record in the canonical
  * insert order (lane, then play order) -- how a test finds one lane's records in M_RL. */
@@ -347,7 +363,7 @@ int nfsp_group_average_ar(nfsp_group* g);
 int nfsp_group_set_timing(nfsp_group* g, int on);
 /* nfsp_engine_get_timings summed over the replicas.  The shared chain and target launches
  * count once each. */
-int nfsp_group_get_timings(nfsp_group* g, double* ms /*[8]*/, int64_t* launches /*[8]*/);
+int nfsp_group_get_timings(nfsp_group* g, double* ms /*[10]*/, int64_t* launches /*[10]*/);
 int nfsp_group_rounds(nfsp_group* g, int64_t* out);   /* BR rounds of the last learner call */
 
 /* ---- evaluation ----

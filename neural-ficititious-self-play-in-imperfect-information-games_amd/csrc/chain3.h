@@ -108,8 +108,9 @@ __device__ inline float sum_x16(float x) {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 #ifdef NFSP_CHAIN_STAMPS
-// diagnostic build: [AR blk 0, AR blk 1, BR, -][wave][phase 0-5, -, -, kernel cycles, steps]
-static __device__ unsigned long long g_chain_stamps[4][4][10];
+// diagnostic build: [RELU * 2 + block][wave][phase 0-5, -, -, kernel cycles, steps] for the
+// one-engine launches (blocks 0, 1); table launches (engine groups) are not stamped
+static __device__ unsigned long long g_chain_stamps[8][4][10];
 #endif
 
 // Stores are unconditional: lanes whose copy is redundant (the odd lane rows of po / dm, the
@@ -494,7 +495,8 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
     if (C.stamps) {
       for (int k = 0; k < 10; ++k) C.stamps[(blockIdx.x * 4 + w) * 10 + k] = st_acc[k];
     } else {       // engine build: accumulate per (net, block, wave) for nfsp_debug_chain_stamps
-      for (int k = 0; k < 10; ++k) atomicAdd(&g_chain_stamps[RELU * 2 + blockIdx.x][w][k], st_acc[k]);
+      if (!TABLE && blockIdx.x < 2)
+        for (int k = 0; k < 10; ++k) atomicAdd(&g_chain_stamps[RELU * 2 + blockIdx.x][w][k], st_acc[k]);
     }
   }
 #endif

@@ -34,7 +34,8 @@ namespace {
 // k_rollout
 // ---------------------------------------------------------------------------
 struct RolloutArgs {
-  int N;
+  int N;                    // lanes of this rollout (one slice)
+  uint32_t lane0;           // global id of the slice's first lane (cfg.slices)
   uint32_t k0, k1;
   uint32_t g_lo, g_hi;      // hand index of this rollout (per lane)
   float eta;
@@ -68,15 +69,16 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& A, int bx) {
   if (tid < 2) s_rew[tid] = 0;
   __syncthreads();
 
-  const int L = bx * blockDim.x + tid;
+  const int L = bx * blockDim.x + tid;     // staging index (lane within the slice)
   if (L < A.N) {
     const int N = A.N;
+    const uint32_t LG = A.lane0 + (uint32_t)L;   // global lane id: Philox counters, dealer
     const double eps0 = A.st->epsilon[0], eps1 = A.st->epsilon[1];
-    const int dealer = (int)((L + A.g_lo) & 1u);
+    const int dealer = (int)((LG + A.g_lo) & 1u);
     const int lhand = 1 - dealer;
     uint8_t r0, r1, rp = 0;
     {
-      const u32x4 u = nfsp::philox4x32({(uint32_t)L, A.g_lo, A.g_hi, 0u}, A.k0, A.k1);
+      const u32x4 u = nfsp::philox4x32({LG, A.g_lo, A.g_hi, 0u}, A.k0, A.k1);
       if (A.game == nfsp::GAME_KUHN)
         nfsp::deal_kuhn(nfsp::below(u.x, 3), nfsp::below(u.y, 2), r0, r1);
       else
@@ -85,7 +87,7 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& A, int bx) {
     // eta draws, dealer first (main.py:36-45): 'a' (AR) iff random() > eta
     int polBR[2];
     {
-      const u32x4 u = nfsp::philox4x32({(uint32_t)L, A.g_lo, A.g_hi, 1u}, A.k0, A.k1);
+      const u32x4 u = nfsp::philox4x32({LG, A.g_lo, A.g_hi, 1u}, A.k0, A.k1);
       polBR[dealer] = !(nfsp::u01(u.x) > A.eta);
       polBR[lhand] = !(nfsp::u01(u.y) > A.eta);
     }
@@ -149,7 +151,7 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& A, int bx) {
         bool fwd = true;
         u32x4 ub{};
         if (br) {                  // act_best_response's eps draw (agent/agent.py:124-128)
-          ub = nfsp::philox4x32({(uint32_t)L, A.g_lo, A.g_hi, 2u + (uint32_t)dec}, A.k0, A.k1);
+          ub = nfsp::philox4x32({LG, A.g_lo, A.g_hi, 2u + (uint32_t)dec}, A.k0, A.k1);
           dec++;
           fwd = (double)nfsp::u01(ub.x) > (p ? eps1 : eps0);
         }
@@ -159,7 +161,7 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& A, int bx) {
           y[0] = nfsp::u01(ub.y); y[1] = nfsp::u01(ub.z); y[2] = nfsp::u01(ub.w);
         }
         if (!br && (A.quirks & NFSP_EXT_SAMPLE_AR)) {   // sample the average policy (textbook NFSP)
-          const u32x4 u = nfsp::philox4x32({(uint32_t)L, A.g_lo, A.g_hi, 0x80000000u + (uint32_t)dec_ar},
+          const u32x4 u = nfsp::philox4x32({LG, A.g_lo, A.g_hi, 0x80000000u + (uint32_t)dec_ar},
                                            A.k0, A.k1);
           dec_ar++;
           const float r = nfsp::u01(u.x);
@@ -216,10 +218,11 @@ __global__ void __launch_bounds__(256) k_rollout(RolloutArgs A) { rollout_body(A
 
 // engine groups: blockIdx.y = replica (the rollout index is the same for every replica)
 __global__ void __launch_bounds__(256) k_rollout_g(const GroupRollout* __restrict__ tab, uint32_t g_lo,
-                                                   uint32_t g_hi) {
+                                                   uint32_t g_hi, uint32_t lane0) {
   RolloutArgs A = tab[blockIdx.y].A;
   A.g_lo = g_lo;
   A.g_hi = g_hi;
+  A.lane0 = lane0;
   rollout_body(A, blockIdx.x);
 }
 
@@ -410,8 +413,7 @@ __global__ void k_finish_rollout(EngineDev* st, int64_t N) {
 }
 
 __global__ void k_finish_rollout_g(const GroupRollout* __restrict__ tab, int R) {
-  const int r = threadIdx.x;
-  if (r < R) {
+  for (int r = threadIdx.x; r < R; r += blockDim.x) {   // R may exceed the block
     EngineDev* st = tab[r].A.st;
     st->hands += tab[r].A.N;
     st->rollouts += 1;
@@ -471,6 +473,7 @@ extern "C" int nfsp_engine_default_cfg(nfsp_engine_cfg* c) {
   c->gamma = 0.95;
   c->epsilon = 0.06;
   c->seed = 1234;
+  c->slices = 1;
   return NFSP_OK;
 }
 
@@ -501,6 +504,8 @@ int engine_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, bool own_streams, n
   NFSP_REQUIRE(ctx && cfg && out, "null argument");
   NFSP_REQUIRE(cfg->hidden == nn::H, "only hidden == 64 is built");
   NFSP_REQUIRE(cfg->n_lanes > 0 && cfg->n_lanes < (1 << 24), "n_lanes must be in [1, 2^24)");
+  NFSP_REQUIRE(cfg->slices >= 1 && cfg->n_lanes % cfg->slices == 0,
+               "slices must be >= 1 and divide n_lanes");
   NFSP_REQUIRE(cfg->fit_batch == CHAIN_MB, "the SGD chains are built for fit_batch == 32");
   NFSP_REQUIRE(cfg->batch >= CHAIN_MB && cfg->batch <= MAX_BATCH && cfg->batch % CHAIN_MB == 0,
                "batch must be 32, 64, 96 or 128");
@@ -519,7 +524,8 @@ int engine_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, bool own_streams, n
   nfsp_engine* e = new nfsp_engine();
   e->ctx = ctx;
   e->cfg = *cfg;
-  e->N = cfg->n_lanes;
+  e->slices = cfg->slices;
+  e->N = cfg->n_lanes / cfg->slices;     // lanes per rollout: staging and learner bounds
   e->nblk = (e->N + 255) / 256;
   const int64_t N = e->N;
   EALLOC(e->w, sizeof(float) * 6 * nn::NP);
@@ -606,10 +612,13 @@ namespace eng {
 static RolloutArgs rollout_args(const nfsp_engine* e) {
   RolloutArgs A;
   A.N = e->N;
+  // the next rollout plays slice rollouts % slices; a lane's hand index is its hand count
+  const uint64_t hand = e->rollouts / (uint64_t)e->slices;
+  A.lane0 = (uint32_t)((e->rollouts % (uint64_t)e->slices) * (uint64_t)e->N);
   A.k0 = (uint32_t)e->cfg.seed;
   A.k1 = (uint32_t)(e->cfg.seed >> 32);
-  A.g_lo = (uint32_t)e->rollouts;
-  A.g_hi = (uint32_t)(e->rollouts >> 32);
+  A.g_lo = (uint32_t)hand;
+  A.g_hi = (uint32_t)(hand >> 32);
   A.eta = e->cfg.eta;
   A.quirks = e->cfg.quirks;
   A.game = e->ctx->game;
@@ -649,7 +658,8 @@ int rollout_launch(nfsp_engine* e) {
 int group_rollout_table(nfsp_engine* const* eng, int R, void** d_tab) {
   std::vector<GroupRollout> h(R);
   for (int r = 0; r < R; ++r) {
-    NFSP_REQUIRE(eng[r]->N == eng[0]->N, "group replicas differ in n_lanes");
+    NFSP_REQUIRE(eng[r]->N == eng[0]->N && eng[r]->slices == eng[0]->slices,
+                 "group replicas differ in n_lanes or slices");
     h[r].A = rollout_args(eng[r]);
     h[r].M = eng[r]->M;
     h[r].nblk = eng[r]->nblk;
@@ -670,7 +680,8 @@ int group_rollout_launch(nfsp_engine* const* eng, int R, const void* d_tab) {
   const GroupRollout* tab = static_cast<const GroupRollout*>(d_tab);
   {
     KTimer kt(e0, KT_ROLLOUT);
-    k_rollout_g<<<dim3(e0->nblk, R), 256, 0, s>>>(tab, (uint32_t)e0->rollouts, (uint32_t)(e0->rollouts >> 32));
+    const RolloutArgs A0 = rollout_args(e0);   // slice and hand index, the same for every replica
+    k_rollout_g<<<dim3(e0->nblk, R), 256, 0, s>>>(tab, A0.g_lo, A0.g_hi, A0.lane0);
   }
   NFSP_LAUNCHED("k_rollout_g");
   {
@@ -684,7 +695,7 @@ int group_rollout_launch(nfsp_engine* const* eng, int R, const void* d_tab) {
     k_commit_g<<<dim3(e0->nblk, R), 256, 0, s>>>(tab);
   }
   NFSP_LAUNCHED("k_commit_g");
-  k_finish_rollout_g<<<1, 64, 0, s>>>(tab, R);
+  k_finish_rollout_g<<<1, 256, 0, s>>>(tab, R);
   NFSP_LAUNCHED("k_finish_rollout_g");
   for (int r = 0; r < R; ++r) {
     eng[r]->rollouts++;
@@ -701,10 +712,15 @@ extern "C" int nfsp_rollout(nfsp_engine* e) {
   return nfsp::eng::rollout_launch(e);
 }
 
+// one hand on every lane: each slice's rollout, then the learner on its inserts
 extern "C" int nfsp_engine_step(nfsp_engine* e) {
-  int rc = nfsp_rollout(e);
-  if (rc != NFSP_OK) return rc;
-  return nfsp_engine_update(e);
+  NFSP_REQUIRE(e, "null argument");
+  for (int k = 0; k < e->slices; ++k) {
+    int rc = nfsp_rollout(e);
+    if (rc != NFSP_OK) return rc;
+    if ((rc = nfsp_engine_update(e)) != NFSP_OK) return rc;
+  }
+  return NFSP_OK;
 }
 
 extern "C" int nfsp_engine_get_stats(nfsp_engine* e, nfsp_engine_stats* out) {

@@ -146,7 +146,9 @@ struct LearnBufs {
 // per-kernel timing slots (nfsp_engine_get_timings)
 enum {
   KT_ROLLOUT = 0, KT_SCAN = 1, KT_COMMIT = 2, KT_LEARNER = 3,   // LEARNER = whole update call
-  KT_PREP = 4, KT_TARGETS = 5, KT_CHAIN_BR = 6, KT_CHAIN_AR = 7, KT_N = 8
+  KT_PREP = 4, KT_TARGETS = 5, KT_CHAIN_BR = 6, KT_CHAIN_AR = 7,
+  KT_BR_STREAM0 = 8, KT_BR_STREAM1 = 9,   // span of agent a's BR stream (first targets .. last chain)
+  KT_N = 10
 };
 
 // Stage packed weights (W1[30][64] | b1 | W2 | b2) into the padded LDS layout of fwd_lds.
@@ -243,7 +245,8 @@ __device__ inline void fwd_lds(const float* __restrict__ sw, uint32_t x, int act
 struct nfsp_engine {
   nfsp_ctx* ctx = nullptr;
   nfsp_engine_cfg cfg{};
-  int N = 0;
+  int N = 0;                   // lanes per rollout (n_lanes / slices)
+  int slices = 1;              // cfg.slices
   int nblk = 0;
   uint64_t rollouts = 0;
   uint32_t learn_tag = 0;

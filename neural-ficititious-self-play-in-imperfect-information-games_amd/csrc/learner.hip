@@ -443,10 +443,10 @@ __global__ void __launch_bounds__(256) k_group_avg_ar(float* const* __restrict__
 }  // namespace
 
 #ifdef NFSP_CHAIN_STAMPS
-// diagnostic build only: the accumulated chain phase cycles ([4][4][10] u64), then reset
+// diagnostic build only: the accumulated chain phase cycles ([8][4][10] u64), then reset
 extern "C" int nfsp_debug_chain_stamps(unsigned long long* out) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_chain_stamps), sizeof(g_chain_stamps)) != hipSuccess) return -1;
-  static const unsigned long long zero[4][4][10] = {};
+  static const unsigned long long zero[8][4][10] = {};
   return hipMemcpyToSymbol(HIP_SYMBOL(g_chain_stamps), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
 }
 #endif
@@ -700,6 +700,7 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
   for (int a = 0; a < 2; ++a) {
     hipStream_t sa = e->s_br[a];
     NFSP_HIP(hipStreamWaitEvent(sa, serial_ar ? ar_done : fork_br, 0));
+    KTimer kspan(e, KT_BR_STREAM0 + a, sa);     // this agent's BR stream, end to end
     for (const Segment& sg : L.seg[a]) {
       {
         KTimer kt2(e, KT_TARGETS, sa);
@@ -888,12 +889,14 @@ static int group_update(nfsp_group* g) {
   for (int r = 0; r < R; ++r) {
     nfsp_engine* e = g->eng[r];
     NFSP_REQUIRE(e->log_loss == loss_log, "the loss log must be on in all replicas of a group or none");
-    e->pending_update = false;
     if ((rc = plan_update(e, g->h_st[r], L[r])) != NFSP_OK) return rc;
     maxU = L[r].maxU > maxU ? L[r].maxU : maxU;
     maxUbr = L[r].maxUbr > maxUbr ? L[r].maxUbr : maxUbr;
     maxSL = L[r].maxSL > maxSL ? L[r].maxSL : maxSL;
   }
+  // every plan succeeded: the rollouts are consumed (a failed plan leaves all of them
+  // pending, so the replicas stay in step)
+  for (int r = 0; r < R; ++r) g->eng[r]->pending_update = false;
   // ---- tables: prep / final args per replica; the AR chains (2R workgroups, one launch);
   // per BR round k the targets and the chain of every (replica, agent) with a k-th segment
   std::vector<ChainJob> ar_jobs;
@@ -1003,6 +1006,7 @@ static int group_update(nfsp_group* g) {
     ar_launched = true;
   }
   NFSP_HIP(hipStreamWaitEvent(g->s_br, fork_br, 0));
+  KTimer kspan(e0, KT_BR_STREAM0, g->s_br);     // the group's one BR stream, end to end
   for (size_t k = 0; k < rounds; ++k) {
     const int nj = (int)(round_off[k + 1] - round_off[k]);
     {
@@ -1071,8 +1075,10 @@ extern "C" int nfsp_group_step(nfsp_group* g) {
   int rc;
   if ((g->flags & NFSP_GROUP_AVG_AR) && !g->w0_valid)      // common AR nets before the first step
     if ((rc = nfsp_group_average_ar(g)) != NFSP_OK) return rc;
-  if ((rc = nfsp::eng::group_rollout_launch(g->eng.data(), g->R, g->d_roll)) != NFSP_OK) return rc;
-  if ((rc = group_update(g)) != NFSP_OK) return rc;
+  for (int k = 0; k < g->eng[0]->slices; ++k) {    // every slice: rollout, then its learner
+    if ((rc = nfsp::eng::group_rollout_launch(g->eng.data(), g->R, g->d_roll)) != NFSP_OK) return rc;
+    if ((rc = group_update(g)) != NFSP_OK) return rc;
+  }
   if (g->flags & NFSP_GROUP_AVG_AR) return nfsp_group_average_ar(g);
   return NFSP_OK;
 }

@@ -9,6 +9,8 @@ agent/agent.py:153).  Configuration keys mirror config.ini:
     reference (config C1)   n_lanes=1,   rl_capacity=40_000,  sl_capacity=40_000
     C2                      n_lanes=65_536
     C3                      n_lanes=1_048_576, rl_capacity=200_000, sl_capacity=2_000_000
+                            (slices=16: the 1M lanes advance in 16 slices of 65,536, the
+                            learner consuming each slice before the next acts)
 """
 from __future__ import annotations
 
@@ -103,6 +105,7 @@ class SelfPlayEngine:
         native.check(self.L.nfsp_engine_update(self.h), "nfsp_engine_update")
 
     def step(self):
+        """One hand on every lane: ``cfg.slices`` x (rollout of the next slice + update)."""
         native.check(self.L.nfsp_engine_step(self.h), "nfsp_engine_step")
 
     def stats(self) -> dict:
@@ -111,15 +114,15 @@ class SelfPlayEngine:
         return s.to_dict()
 
     KERNELS = ("k_rollout", "k_scan", "k_commit", "learner", "learner_prep", "k_br_targets",
-               "k_chain3_br", "k_chain3_ar")
+               "k_chain3_br", "k_chain3_ar", "br_stream_a0", "br_stream_a1")
 
     def set_timing(self, on=True):
         native.check(self.L.nfsp_engine_set_timing(self.h, int(bool(on))), "set_timing")
 
     def timings(self) -> dict:
         """{kernel: (total ms, launches)} since the last call (HIP events, ctx stream)."""
-        ms = (native.F64 * 8)()
-        n = (native.I64 * 8)()
+        ms = (native.F64 * len(self.KERNELS))()
+        n = (native.I64 * len(self.KERNELS))()
         native.check(self.L.nfsp_engine_get_timings(self.h, ms, n), "get_timings")
         return {k: (ms[i], n[i]) for i, k in enumerate(self.KERNELS)}
 
@@ -143,7 +146,7 @@ class SelfPlayEngine:
             sl_s=_wrap_device(sl.s, sl.cap * 30, torch.float32, d, self).view(sl.cap, 30),
             sl_a=_wrap_device(sl.a, sl.cap * 3, torch.float32, d, self).view(sl.cap, 3),
         )
-        pc = 4 * self.cfg.n_lanes
+        pc = 4 * self.slice_lanes
         out["pend_x"] = _wrap_device(px.value, pc, torch.int32, d, self)
         out["pend_a"] = _wrap_device(pa.value, pc * 3, torch.float32, d, self).view(pc, 3)
         out["pend_pos"] = _wrap_device(pp.value, pc, torch.int64, d, self)
@@ -157,13 +160,25 @@ class SelfPlayEngine:
         return (_wrap_device(rows.value, B, torch.int64, self.dev).cpu().numpy(),
                 _wrap_device(perms.value, E * B, torch.int32, self.dev).view(E, B).cpu().numpy())
 
+    @property
+    def slice_lanes(self) -> int:
+        """Lanes per rollout (cfg.slices: n_lanes / slices)."""
+        return self.cfg.n_lanes // self.cfg.slices
+
+    def last_slice(self) -> tuple:
+        """(global id of the first lane, hand index g) of the last rollout: rollout k plays
+        slice k % slices with the lanes' hand index k // slices (include/nfsp.h cfg.slices)."""
+        k = self.stats()["rollouts"] - 1
+        return (k % self.cfg.slices) * self.slice_lanes, k // self.cfg.slices
+
     def lane_counts(self) -> np.ndarray:
-        """[n_lanes, 4] (RL agent 0, RL agent 1, SL agent 0, SL agent 1) records of each lane's
-        hand in the last rollout (nfsp_engine_lane_counts; synchronises)."""
+        """[n_lanes / slices, 4] (RL agent 0, RL agent 1, SL agent 0, SL agent 1) records of each
+        lane's hand in the last rollout (its slice's lanes; nfsp_engine_lane_counts;
+        synchronises)."""
         p = native.P()
         native.check(self.L.nfsp_engine_lane_counts(self.h, C.byref(p)), "lane_counts")
         torch.cuda.synchronize(self.dev)
-        c = _wrap_device(p.value, self.cfg.n_lanes, torch.int32, self.dev).cpu().numpy()
+        c = _wrap_device(p.value, self.slice_lanes, torch.int32, self.dev).cpu().numpy()
         c = c.astype(np.int64) & 0xFFFF
         return np.stack([(c >> (4 * k)) & 15 for k in range(4)], axis=1)
 
@@ -262,8 +277,8 @@ class EngineGroup:
         native.check(self.L.nfsp_group_set_timing(self.h, int(bool(on))), "set_timing")
 
     def timings(self) -> dict:
-        ms = (native.F64 * 8)()
-        n = (native.I64 * 8)()
+        ms = (native.F64 * len(self.KERNELS))()
+        n = (native.I64 * len(self.KERNELS))()
         native.check(self.L.nfsp_group_get_timings(self.h, ms, n), "get_timings")
         return {k: (ms[i], n[i]) for i, k in enumerate(self.KERNELS)}
 

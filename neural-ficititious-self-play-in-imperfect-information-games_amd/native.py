@@ -39,7 +39,7 @@ class EngineCfg(C.Structure):
                 ("sl_capacity", I64), ("batch", C.c_int32), ("inserts_per_update", C.c_int32),
                 ("target_every", C.c_int32), ("epochs", C.c_int32), ("fit_batch", C.c_int32),
                 ("quirks", C.c_uint32), ("eta", F32), ("lr_br", F32), ("lr_ar", F32),
-                ("gamma", F64), ("epsilon", F64), ("seed", U64)]
+                ("gamma", F64), ("epsilon", F64), ("seed", U64), ("slices", C.c_int32)]
 
 
 class EngineStats(C.Structure):

@@ -16,6 +16,8 @@ reference are the ones the engine declares (include/nfsp.h, nfsp_engine section)
               x -> eps draw (BR net iff u01 > eps), (y, z, w) -> np.random.rand(1,1,3)
   with below(u, n) = (u * n) >> 32 and u01(u) = (u >> 8) * 2^-24;
 * dealer of lane L in rollout g = (L + g) & 1 (the reference alternates per hand);
+* lane slices (nfsp_engine_cfg.slices): a rollout plays lanes [lane0, lane0 + n_lanes) of
+  the engine's global lane ids, and g is the lanes' hand count (rollouts // slices);
 * no updates inside the rollout (the engine's learner runs after it).
 
 Records come out per agent in the engine's canonical order: lane ascending, then play
@@ -91,10 +93,11 @@ def orc_bits(x) -> int:
 
 
 def rollout_with_positions(n_lanes, g, seed, w_flat, eps, eta=0.1, alias=True, rl_before=(0, 0),
-                           game="leduc", ext=0):
+                           game="leduc", ext=0, lane0=0):
     """rollout() plus, for each SL record, its global RL stream position (what the engine
-    stores in its pending list).  ``ext``: the engine's NFSP_EXT_* bits (include/nfsp.h)."""
-    out = rollout_lanes(n_lanes, g, seed, w_flat, eps, eta, alias, game, ext)
+    stores in its pending list).  ``ext``: the engine's NFSP_EXT_* bits (include/nfsp.h).
+    ``lane0``: global id of the first lane (a slice of a sliced engine)."""
+    out = rollout_lanes(n_lanes, g, seed, w_flat, eps, eta, alias, game, ext, lane0)
     rl = ([], [])
     sl = ([], [])
     base = list(rl_before)
@@ -107,12 +110,12 @@ def rollout_with_positions(n_lanes, g, seed, w_flat, eps, eta=0.1, alias=True, r
     return dict(rl=rl, sl=sl, actions=out["actions"], reward=out["reward"])
 
 
-def rollout_lanes(n_lanes, g, seed, w_flat, eps, eta=0.1, alias=True, game="leduc", ext=0):
-    """Like rollout() but keeps the records per lane."""
+def rollout_lanes(n_lanes, g, seed, w_flat, eps, eta=0.1, alias=True, game="leduc", ext=0, lane0=0):
+    """Like rollout() but keeps the records per lane (global lanes lane0 .. lane0 + n_lanes)."""
     lanes = []
     actions = np.zeros((2, 3), np.int64)
     reward = np.zeros(2)
-    for L in range(n_lanes):
+    for L in range(lane0, lane0 + n_lanes):
         res = _one_lane(L, g, seed, w_flat, eps, eta, alias, game, ext)
         lanes.append(res)
         actions += res["actions"]

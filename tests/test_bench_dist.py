@@ -77,6 +77,19 @@ def test_world_size_mismatch_refused():
     assert "WORLD_SIZE 1 != --gpus 2" in err
 
 
+def test_failing_rank_ends_the_job_fast():
+    """A rank that dies (here: rank 1 exits 3 once the group is up) ends the whole job with its
+    exit code within seconds: the launcher stops rank 0, which is blocked in the timed
+    region's barrier, instead of waiting for the process-group timeout."""
+    t0 = time.time()
+    rc, lines, err = _bench(["--gpus", "2", "--steps", "50", "--warmup", "1", "--stub-step-ms", "20",
+                             "--stub-fail", "1:3"], env_extra={"NFSP_PG_TIMEOUT_S": "600"})
+    assert rc == 3, err
+    assert not lines
+    assert "rank 1 exited with 3" in err
+    assert time.time() - t0 < 60
+
+
 def test_two_rank_timing_protocol():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

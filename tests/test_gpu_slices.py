@@ -1,0 +1,152 @@
+"""Lane slices (nfsp_engine_cfg.slices): C3's 1,048,576 envs advanced in 16 slices of 65,536,
+the learner consuming each slice's inserts before the next slice acts.  That bounds the
+engine's declared policy lag (include/nfsp.h) by one slice instead of one million hands, so
+C3 learns at the rate of the reference's one-hand-at-a-time main.train (main.py:27-67,
+update trigger agent/agent.py:153-154).
+
+* a lane's hand does not depend on the slicing (Philox counters and the dealer use the
+  global lane id and the lane's hand count): with the learner off, a sliced engine fills
+  M_RL and M_SL exactly like an unsliced one, record for record;
+* at C3 size with the learner on, sampled lanes of the sliced rollouts replay bit-exact
+  through oracle/rollout_oracle.py (global lane ids, hand index = rollouts // slices);
+* the C3 learning gate: exact exploitability after 8M / 16M / 25M / 33M hands at C3 (1M
+  lanes, 16 slices, M_RL 200k, M_SL 2M) against the CPU seed band of the reference's
+  main.train restated in C++ with the same memories and initial nets
+  (tests/golden/cpu_band_c3mem.json).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import rollout_oracle as R
+from test_gpu_fullsize import _bits_dev, _sample_lanes, _weights_flat
+
+pytestmark = pytest.mark.gpu
+
+C3 = dict(n_lanes=1_048_576, rl_capacity=200_000, sl_capacity=2_000_000)
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _logical_rl(eng, p):
+    """M_RL as the reference's deque: the last min(total, capacity) records, oldest first."""
+    st = eng.stats()
+    m = eng.memories(p)
+    tot = int(st["rl_total"][p])
+    n = min(tot, int(eng.cfg.rl_capacity))
+    rows = torch.arange(tot - n, tot, device=m["rl_s"].device) % m["log_cap"]
+    return {k: m[k][rows].cpu().numpy() for k in ("rl_s", "rl_a", "rl_r", "rl_s2", "rl_t")}
+
+
+def test_slicing_leaves_every_hand_unchanged(pkg):
+    """Learner off: 4 slices of 2,048 lanes fill the memories exactly like 8,192 lanes at once."""
+    kw = dict(n_lanes=8192, rl_capacity=20_000, sl_capacity=3_000, seed=99, init_seed=3,
+              inserts_per_update=1 << 30)
+    a = pkg.engine.SelfPlayEngine(**kw)
+    b = pkg.engine.SelfPlayEngine(slices=4, **kw)
+    for _ in range(3):                 # M_RL wraps, the reservoir replaces
+        a.step()
+        b.step()
+    sa, sb = a.stats(), b.stats()
+    assert sb["rollouts"] == 4 * sa["rollouts"] == 12
+    for k in ("hands", "rl_total", "sl_total", "rl_size", "sl_size", "actions", "reward"):
+        assert sa[k] == sb[k], k
+    assert sa["sl_total"][0] > kw["sl_capacity"] and sa["rl_total"][0] > kw["rl_capacity"]
+    for p in (0, 1):
+        ma, mb = _logical_rl(a, p), _logical_rl(b, p)
+        for k in ma:
+            assert np.array_equal(ma[k], mb[k]), (p, k)
+        n = int(sa["sl_size"][p])
+        xa, xb = a.memories(p), b.memories(p)
+        assert np.array_equal(xa["sl_s"][:n].cpu().numpy(), xb["sl_s"][:n].cpu().numpy())
+        assert np.array_equal(xa["sl_a"][:n].cpu().numpy(), xb["sl_a"][:n].cpu().numpy())
+
+
+def _check_slice_lanes(eng, seed, lanes, rl_before):
+    """Sampled local lanes of the last rollout vs the oracle's replay of their global lanes."""
+    lane0, g = eng.last_slice()
+    st = eng.stats()
+    cnt = eng.lane_counts()
+    assert len(cnt) == eng.slice_lanes
+    assert cnt[:, 0].sum() == st["last_rl"][0] and cnt[:, 1].sum() == st["last_rl"][1]
+    pre = np.zeros_like(cnt)
+    pre[1:] = np.cumsum(cnt, axis=0)[:-1]
+    w = _weights_flat(eng)
+    eps = (float(st["epsilon"][0]), float(st["epsilon"][1]))
+    mems = [eng.memories(p) for p in (0, 1)]
+    for L in lanes:
+        ref = R._one_lane(lane0 + L, g, seed, w, eps, eng.cfg.eta, True)
+        for p in (0, 1):
+            m = mems[p]
+            n = len(ref["rl"][p])
+            assert cnt[L, p] == n, (L, p)
+            if n:
+                rows = torch.tensor((rl_before[p] + pre[L, p] + np.arange(n)) % m["log_cap"],
+                                    dtype=torch.int64, device=m["rl_s"].device)
+                exp = ref["rl"][p]
+                assert np.array_equal(_bits_dev(m["rl_s"][rows]), [e[0] for e in exp]), (L, p)
+                assert np.array_equal(_bits_dev(m["rl_s2"][rows]), [e[3] for e in exp]), (L, p)
+                assert np.abs(m["rl_a"][rows].cpu().numpy() - np.array([e[1] for e in exp])).max() <= 1e-6
+                assert np.array_equal(m["rl_r"][rows].cpu().numpy(), np.array([e[2] for e in exp], np.float32))
+            k = len(ref["sl"][p])
+            assert cnt[L, 2 + p] == k, (L, p)
+            if k:
+                q = slice(int(pre[L, 2 + p]), int(pre[L, 2 + p]) + k)
+                px = m["pend_x"][q].cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+                assert np.array_equal(px, [e[0] for e in ref["sl"][p]]), (L, p)
+                pos = m["pend_pos"][q].cpu().numpy()
+                assert np.array_equal(pos, [rl_before[p] + pre[L, p] + e[2] for e in ref["sl"][p]])
+
+
+def test_c3_sliced_rollouts_replay_on_the_oracle(pkg):
+    """C3 at 16 slices, learner on: after one whole step (16 learner calls), the next two
+    slices' sampled lanes replay bit-exact with their global lane ids and hand index 1."""
+    seed = 2468
+    eng = pkg.engine.SelfPlayEngine(seed=seed, init_seed=4, slices=16, **C3)
+    eng.step()
+    st = eng.stats()
+    assert st["hands"] == C3["n_lanes"] and st["rollouts"] == 16
+    assert min(st["br_updates"]) > 1000            # the learner ran between the slices
+    S = eng.slice_lanes
+    for k in range(2):
+        before = tuple(int(v) for v in eng.stats()["rl_total"])
+        eng.rollout()
+        assert eng.last_slice() == (k * S, 1)
+        _check_slice_lanes(eng, seed, _sample_lanes(S, 48, 10 + k), before)
+        eng.update()
+
+
+def _band():
+    with open(os.path.join(HERE, "golden", "cpu_band_c3mem.json")) as f:
+        return json.load(f)
+
+
+def test_c3_sliced_learns_within_the_cpu_seed_band(pkg):
+    """BASELINE.json's second metric at C3: the exploitability-vs-hands curve of the 1M-lane
+    engine (16 slices) lies within the CPU reference's seed band."""
+    band = _band()
+    cpu = {int(h): np.array(v) for h, v in band["curves_by_hands"].items()}
+    seeds = band["seeds"]
+    checkpoints = (8, 16, 24, 32)                  # engine steps of 1,048,576 hands
+    gpu = {c: [] for c in checkpoints}
+    for s in seeds:
+        eng = pkg.engine.SelfPlayEngine(seed=1234 + s, init_seed=s, slices=16, **C3)
+        for k in range(1, checkpoints[-1] + 1):
+            eng.step()
+            if k in gpu:
+                gpu[k].append(eng.exploitability(0)["exploitability"])
+        eng.close()
+        del eng
+        torch.cuda.empty_cache()
+    report = []
+    for k in checkpoints:
+        h = k * C3["n_lanes"]
+        near = min(cpu, key=lambda x: abs(x - h))  # the CPU checkpoint (every 2M hands) nearest
+        cm, cs = float(cpu[near].mean()), float(cpu[near].std())
+        gm, gs = float(np.mean(gpu[k])), float(np.std(gpu[k]))
+        report.append((h, near, round(cm, 3), round(cs, 3), round(gm, 3), round(gs, 3)))
+    print("hands, cpu checkpoint, cpu mean, cpu std, gpu mean, gpu std:", report)
+    for (h, near, cm, cs, gm, gs) in report:
+        assert abs(gm - cm) <= 2 * cs, report

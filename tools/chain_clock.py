@@ -44,7 +44,7 @@ def main():
     eng = pkg.engine.SelfPlayEngine(n_lanes=args.lanes, rl_capacity=200_000, sl_capacity=2_000_000, seed=1234)
     L = C.CDLL(lib)
     L.nfsp_debug_chain_stamps.argtypes = [C.c_void_p]
-    buf = (C.c_ulonglong * 160)()
+    buf = (C.c_ulonglong * 320)()          # [8][4][10]: RELU * 2 + block
     for _ in range(2):
         eng.step()
     torch.cuda.synchronize()
