@@ -360,6 +360,9 @@ def main():
     ap.add_argument("--stub-step-ms", type=float, default=None, help=argparse.SUPPRESS)
     # test hook with --stub-step-ms: rank R exits with code C after the process group is up
     ap.add_argument("--stub-fail", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--slices", type=int, default=None, help="override the config's lane slices")
+    ap.add_argument("--slice-lag", type=int, default=None, choices=[1, 2],
+                    help="override the config's slice lag (2: slices pipelined)")
     ap.add_argument("--groups", default="c3_r4,c3_r16,c3_r64,c3_r256",
                     help="engine-group configs measured beside the C3 headline at N = 1 "
                          "(`groups` in the JSON line; '' = none)")
@@ -381,7 +384,11 @@ def main():
 
     import __graft_entry__
     pkg = __graft_entry__.load_package()
-    cfg = CONFIGS[args.config]
+    cfg = dict(CONFIGS[args.config])
+    for k, v in (("slices", args.slices), ("slice_lag", args.slice_lag)):
+        if v is not None:
+            cfg[k] = v
+            cfg["label"] += f" [{k} {v}]"
     game = pkg.native.GAME_KUHN if cfg.get("game") == "kuhn" else pkg.native.GAME_LEDUC
     R = cfg.get("replicas", 1)
     if R > 1:        # seeds 1234 + R rank + r: distinct over every replica of the job
@@ -389,7 +396,7 @@ def main():
                                      sl_capacity=cfg["sl_capacity"], seed=1234 + R * rank,
                                      init_seed=R * rank, game=game, avg_ar=True)
     else:
-        extra = {k: cfg[k] for k in ("quirks", "slices") if k in cfg}
+        extra = {k: cfg[k] for k in ("quirks", "slices", "slice_lag") if k in cfg}
         eng = pkg.engine.SelfPlayEngine(n_lanes=cfg["n_lanes"], rl_capacity=cfg["rl_capacity"],
                                         sl_capacity=cfg["sl_capacity"], seed=1234 + rank,
                                         init_seed=rank, game=game, **extra)
@@ -550,6 +557,7 @@ def main():
         "kernel_ms_source": "HIP events around every launch, second pass of K steps",
         "stream_ms_per_step": streams,
         "slices": cfg.get("slices", 1),
+        "slice_lag": cfg.get("slice_lag", 1),
         "rollout_only_hands_per_s": cfg["n_lanes"] / (rollout_path_ms * 1e-3) * world,
         "per_step": {"br_updates": br_upd / args.steps, "ar_updates": ar_upd / args.steps,
                      "rl_inserts_per_hand": t_rl, "sl_inserts_per_hand": t_sl},

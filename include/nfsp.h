@@ -255,6 +255,15 @@ typedef struct nfsp_engine_cfg {
    * lane's hand does not depend on the slicing.  Staging and learner buffers are sized for
    * one slice.  n_lanes must be a multiple of slices. */
   int32_t slices;
+  /* Slice lag inside nfsp_engine_step (slices > 1): 1 = the learner of slice k completes
+   * before slice k + 1 acts; 2 = pipelined: slice k + 1's rollout (and the host's plan and the
+   * prep kernels of its learner) run while slice k's SGD chains do, so slice k + 1 acts with
+   * the nets and epsilon as of the end of slice k - 1's learner (the first two slices of a step:
+   * as of the step's start).  The policy lag is then two slices; the chains' streams never
+   * wait for a rollout.  Each step starts from the nets as they are (nfsp_engine_weights
+   * writes between steps are seen) and ends with every stream joined.  nfsp_rollout /
+   * nfsp_engine_update called by themselves always run with lag 1.  Engine groups: 1 only. */
+  int32_t slice_lag;
 } nfsp_engine_cfg;
 
 typedef struct nfsp_engine_stats {
@@ -327,6 +336,11 @@ int nfsp_engine_last_update(nfsp_engine* e, int agent, int role, int64_t** dev_r
  * hand).  Their exclusive prefix over lanes is each lane's first record in the canonical
  * insert order (lane, then play order) -- how a test finds one lane's records in M_RL. */
 int nfsp_engine_lane_counts(nfsp_engine* e, uint32_t** dev_counts);
+
+/* Debug view (cfg.slice_lag 2): the acting nets [2 agents][3 nets][NP] (target slots unused)
+ * and epsilons of snapshot `parity` -- after a pipelined nfsp_engine_step of K slices, snapshot
+ * (K - 1) & 1 holds what the step's last slice acted with. */
+int nfsp_engine_snapshot(nfsp_engine* e, int parity, float** dev_w, double* eps /*[2]*/);
 
 /* Test hook: from the next nfsp_engine_update on, each agent's AR and BR chains run only the
  * first max_updates updates of the learner call (0 = all).  Everything else still follows

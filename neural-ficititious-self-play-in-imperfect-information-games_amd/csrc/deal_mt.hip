@@ -87,6 +87,9 @@ struct Mt19937 {
 struct DealMt {
   Mt19937 mt;
   int mode = NFSP_DEAL_PHILOX;
+  uint8_t* staging = nullptr;       // pinned [n_envs][3]: one reset's deals
+  hipEvent_t copied = nullptr;      // the last staging -> device copy
+  bool in_flight = false;
 };
 
 // one reset's deal: shuffle the ordered deck (card c = rank c >> 1, suit c & 1;
@@ -105,19 +108,33 @@ static void draw_deal(DealMt& d, uint8_t out[3]) {
   out[2] = (uint8_t)(cards[3] >> 1);
 }
 
-// nfsp_env_reset's host part in an MT deal mode: the ctx's next n deals into pending_deal
+// nfsp_env_reset's host part in an MT deal mode: the ctx's next n deals into pending_deal,
+// through a pinned staging buffer.  Only the previous reset's copy out of that buffer is
+// waited for (its event), not the whole stream.
 int deal_mt_stage(nfsp_ctx* c) {
   DealMt& d = *static_cast<DealMt*>(c->deal_mt);
-  std::vector<uint8_t> h(3 * (size_t)c->n_envs);
-  for (int i = 0; i < c->n_envs; ++i) draw_deal(d, &h[3 * (size_t)i]);
-  NFSP_HIP(hipMemcpyAsync(c->pending_deal, h.data(), h.size(), hipMemcpyHostToDevice, c->stream));
-  NFSP_HIP(hipStreamSynchronize(c->stream));      // h is pageable and goes out of scope
+  const size_t bytes = 3 * (size_t)c->n_envs;
+  if (!d.staging) {
+    NFSP_HIP(hipHostMalloc((void**)&d.staging, bytes, hipHostMallocDefault));
+    NFSP_HIP(hipEventCreateWithFlags(&d.copied, hipEventDisableTiming));
+  }
+  if (d.in_flight) NFSP_HIP(hipEventSynchronize(d.copied));
+  for (int i = 0; i < c->n_envs; ++i) draw_deal(d, d.staging + 3 * (size_t)i);
+  NFSP_HIP(hipMemcpyAsync(c->pending_deal, d.staging, bytes, hipMemcpyHostToDevice, c->stream));
+  NFSP_HIP(hipEventRecord(d.copied, c->stream));
+  d.in_flight = true;
   c->has_pending_deal = true;
   return NFSP_OK;
 }
 
 void deal_mt_free(nfsp_ctx* c) {
-  delete static_cast<DealMt*>(c->deal_mt);
+  DealMt* d = static_cast<DealMt*>(c->deal_mt);
+  if (d) {
+    if (d->in_flight) (void)hipEventSynchronize(d->copied);
+    if (d->copied) (void)hipEventDestroy(d->copied);
+    if (d->staging) (void)hipHostFree(d->staging);
+  }
+  delete d;
   c->deal_mt = nullptr;
 }
 

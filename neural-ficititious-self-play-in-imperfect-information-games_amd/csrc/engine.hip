@@ -41,7 +41,9 @@ struct RolloutArgs {
   float eta;
   unsigned quirks;
   int game;                 // nfsp::GAME_LEDUC | GAME_KUHN
-  const float* w;           // [2][3][NP]
+  int eps_by_value;         // 1: eps_v (the host's schedule mirror); 0: st->epsilon (groups)
+  double eps_v[2];
+  const float* w;           // [2][3][NP]: the acting nets (the engine's, or a snapshot)
   EngineDev* st;
   Staging S;
 };
@@ -73,7 +75,8 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& A, int bx) {
   if (L < A.N) {
     const int N = A.N;
     const uint32_t LG = A.lane0 + (uint32_t)L;   // global lane id: Philox counters, dealer
-    const double eps0 = A.st->epsilon[0], eps1 = A.st->epsilon[1];
+    const double eps0 = A.eps_by_value ? A.eps_v[0] : A.st->epsilon[0];
+    const double eps1 = A.eps_by_value ? A.eps_v[1] : A.st->epsilon[1];
     const int dealer = (int)((LG + A.g_lo) & 1u);
     const int lhand = 1 - dealer;
     uint8_t r0, r1, rp = 0;
@@ -474,6 +477,7 @@ extern "C" int nfsp_engine_default_cfg(nfsp_engine_cfg* c) {
   c->epsilon = 0.06;
   c->seed = 1234;
   c->slices = 1;
+  c->slice_lag = 1;
   return NFSP_OK;
 }
 
@@ -485,6 +489,9 @@ extern "C" int nfsp_engine_destroy(nfsp_engine* e) {
   for (hipStream_t st : {e->s_br[0], e->s_br[1], e->s_ar})
     if (st) (void)hipStreamSynchronize(st);
   for (void* p : e->allocs) (void)hipFree(p);
+  for (auto& pe : e->snap_ev)
+    for (hipEvent_t ev : pe)
+      if (ev) (void)hipEventDestroy(ev);
   for (auto& m : e->marks) {
     e->pool.push_back(m.second.first);
     e->pool.push_back(m.second.second);
@@ -506,6 +513,8 @@ int engine_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, bool own_streams, n
   NFSP_REQUIRE(cfg->n_lanes > 0 && cfg->n_lanes < (1 << 24), "n_lanes must be in [1, 2^24)");
   NFSP_REQUIRE(cfg->slices >= 1 && cfg->n_lanes % cfg->slices == 0,
                "slices must be >= 1 and divide n_lanes");
+  NFSP_REQUIRE(cfg->slice_lag == 1 || cfg->slice_lag == 2, "slice_lag must be 1 or 2");
+  NFSP_REQUIRE(cfg->slice_lag == 1 || own_streams, "engine groups run with slice_lag 1");
   NFSP_REQUIRE(cfg->fit_batch == CHAIN_MB, "the SGD chains are built for fit_batch == 32");
   NFSP_REQUIRE(cfg->batch >= CHAIN_MB && cfg->batch <= MAX_BATCH && cfg->batch % CHAIN_MB == 0,
                "batch must be 32, 64, 96 or 128");
@@ -556,20 +565,43 @@ int engine_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, bool own_streams, n
   EALLOC(e->M.dbg_rows, 8 * 4 * cfg->batch);
   EALLOC(e->M.dbg_perms, 4 * 4 * 4 * cfg->batch);
   // learner: <= 4N RL inserts per agent per rollout -> <= 4N / c + 2 update triggers
-  LearnBufs& L = e->LB;
-  L.umax = 4 * N / cfg->inserts_per_update + 2;
-  const int64_t ub = 2 * L.umax * cfg->batch, ueb = ub * cfg->epochs;
-  EALLOC(L.br_rows, sizeof(BrRow) * ub);
-  EALLOC(L.br_perm, ueb);
-  EALLOC(L.br_expl, sizeof(double) * 2 * L.umax);
-  EALLOC(L.br_rec, sizeof(StepRec) * (ueb / CHAIN_MB));
-  EALLOC(L.ar_rec, sizeof(StepRec) * (ueb / CHAIN_MB));
-  EALLOC(L.ar_active, 2 * L.umax);
-  EALLOC(L.br_loss, 4 * 2 * L.umax * cfg->epochs);
-  EALLOC(L.ar_loss, 4 * 2 * L.umax * cfg->epochs);
-  EALLOC(L.res_head, sizeof(unsigned long long) * sc);
-  EALLOC(L.res_next, 4 * pc);
-  EALLOC(L.res_slot, 4 * pc);
+  // (cfg.slice_lag 2: two sets, slice parity; the reservoir lists are shared -- only the
+  // ctx stream's prep kernels use them, in slice order)
+  e->slice_lag = cfg->slice_lag;
+  for (int k = 0; k < (e->slice_lag == 2 ? 2 : 1); ++k) {
+    LearnBufs& L = e->LBs[k];
+    L.umax = 4 * N / cfg->inserts_per_update + 2;
+    const int64_t ub = 2 * L.umax * cfg->batch, ueb = ub * cfg->epochs;
+    EALLOC(L.br_rows, sizeof(BrRow) * ub);
+    EALLOC(L.br_perm, ueb);
+    EALLOC(L.br_expl, sizeof(double) * 2 * L.umax);
+    EALLOC(L.br_rec, sizeof(StepRec) * (ueb / CHAIN_MB));
+    EALLOC(L.ar_rec, sizeof(StepRec) * (ueb / CHAIN_MB));
+    EALLOC(L.ar_active, 2 * L.umax);
+    EALLOC(L.br_loss, 4 * 2 * L.umax * cfg->epochs);
+    EALLOC(L.ar_loss, 4 * 2 * L.umax * cfg->epochs);
+    if (k == 0) {
+      EALLOC(L.res_head, sizeof(unsigned long long) * sc);
+      EALLOC(L.res_next, 4 * pc);
+      EALLOC(L.res_slot, 4 * pc);
+    } else {
+      L.res_head = e->LBs[0].res_head;
+      L.res_next = e->LBs[0].res_next;
+      L.res_slot = e->LBs[0].res_slot;
+    }
+  }
+  e->LB = e->LBs[0];
+  if (e->slice_lag == 2) {
+    EALLOC(e->snap, sizeof(float) * 2 * 6 * nn::NP);
+    for (auto& pe : e->snap_ev)
+      for (hipEvent_t& ev : pe) {
+        const hipError_t er = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        if (er != hipSuccess) {
+          nfsp_engine_destroy(e);
+          return nfsp::hip_fail(er, "nfsp_engine_create: hipEventCreate");
+        }
+      }
+  }
   for (hipStream_t* st : {&e->s_br[0], &e->s_br[1], &e->s_ar}) {
     if (!own_streams) break;
     hipError_t sr = hipStreamCreateWithFlags(st, hipStreamNonBlocking);
@@ -583,6 +615,7 @@ int engine_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, bool own_streams, n
     h.epsilon[a] = cfg->epsilon;
     h.temp[a] = 1.0;
     h.lr_br[a] = cfg->lr_br;
+    e->hs.epsilon[a] = cfg->epsilon;
   }
   hipError_t r = hipMemcpyAsync(e->st, &h, sizeof(h), hipMemcpyHostToDevice, ctx->stream);
   if (r == hipSuccess) r = hipStreamSynchronize(ctx->stream);
@@ -612,6 +645,8 @@ namespace eng {
 static RolloutArgs rollout_args(const nfsp_engine* e) {
   RolloutArgs A;
   A.N = e->N;
+  A.eps_by_value = 0;               // groups: each replica's st->epsilon (static table)
+  A.eps_v[0] = A.eps_v[1] = 0.0;
   // the next rollout plays slice rollouts % slices; a lane's hand index is its hand count
   const uint64_t hand = e->rollouts / (uint64_t)e->slices;
   A.lane0 = (uint32_t)((e->rollouts % (uint64_t)e->slices) * (uint64_t)e->N);
@@ -628,10 +663,16 @@ static RolloutArgs rollout_args(const nfsp_engine* e) {
   return A;
 }
 
-int rollout_launch(nfsp_engine* e) {
+int rollout_launch(nfsp_engine* e) { return rollout_launch_with(e, e->w, e->hs.epsilon); }
+
+int rollout_launch_with(nfsp_engine* e, const float* w, const double eps[2]) {
   NFSP_REQUIRE(!e->pending_update, "nfsp_engine_update must consume the previous rollout first");
   hipStream_t s = e->ctx->stream;
-  const RolloutArgs A = rollout_args(e);
+  RolloutArgs A = rollout_args(e);
+  A.w = w;
+  A.eps_by_value = 1;               // the schedule as the host computed it (= st->epsilon)
+  A.eps_v[0] = eps[0];
+  A.eps_v[1] = eps[1];
   {
     KTimer kt(e, KT_ROLLOUT);
     k_rollout<<<e->nblk, 256, 0, s>>>(A);
@@ -715,6 +756,7 @@ extern "C" int nfsp_rollout(nfsp_engine* e) {
 // one hand on every lane: each slice's rollout, then the learner on its inserts
 extern "C" int nfsp_engine_step(nfsp_engine* e) {
   NFSP_REQUIRE(e, "null argument");
+  if (e->slice_lag == 2 && e->slices > 1 && e->s_ar) return nfsp::eng::step_pipelined(e);
   for (int k = 0; k < e->slices; ++k) {
     int rc = nfsp_rollout(e);
     if (rc != NFSP_OK) return rc;

@@ -255,7 +255,20 @@ struct nfsp_engine {
   nfsp::eng::EngineDev* st = nullptr;
   nfsp::eng::Staging S{};
   nfsp::eng::Memories M{};
-  nfsp::eng::LearnBufs LB{};
+  nfsp::eng::LearnBufs LB{};        // the learner call's buffers: LBs[parity of the slice]
+  nfsp::eng::LearnBufs LBs[2]{};     // [1] only with cfg.slice_lag 2 (double-buffered slices)
+  int slice_lag = 1;                 // cfg.slice_lag
+  // cfg.slice_lag 2: the acting nets of the next rollouts, [parity][2 agents][3 nets][NP]
+  // (target slots unused), and the epsilon each parity's rollout acts with
+  float* snap = nullptr;
+  double snap_eps[2][2] = {};
+  hipEvent_t snap_ev[2][3] = {};     // [parity][AR stream, BR stream 0, BR stream 1]
+  // host mirror of the schedules (agent/agent.py:245-253, 266-273): plan_update computes them
+  // in the reference's double arithmetic; k_finalize publishes them to EngineDev for the stats
+  struct Sched {
+    int64_t iteration[2], target_count[2], target_syncs[2];
+    double epsilon[2];
+  } hs{};
   hipStream_t s_br[2] = {nullptr, nullptr};
   hipStream_t s_ar = nullptr;
   std::vector<void*> allocs;
@@ -274,6 +287,10 @@ namespace eng {
 hipEvent_t take_event(nfsp_engine* e);
 int engine_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, bool own_streams, nfsp_engine** out);
 int rollout_launch(nfsp_engine* e);   // nfsp_rollout's launches
+// the same with the acting nets / epsilon given (cfg.slice_lag 2: a snapshot)
+int rollout_launch_with(nfsp_engine* e, const float* w, const double eps[2]);
+// nfsp_engine_step with cfg.slice_lag 2 (learner.hip): the slices pipelined
+int step_pipelined(nfsp_engine* e);
 // engine groups: the replicas' rollout arguments as a device table (static), and every
 // replica's rollout through it in one launch per kernel
 int group_rollout_table(nfsp_engine* const* eng, int R, void** d_tab);

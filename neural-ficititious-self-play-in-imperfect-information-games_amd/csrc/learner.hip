@@ -393,16 +393,20 @@ struct FinalArgs {
   int64_t sl_cap;
 };
 
+// mode bits: 1 = the insert counters (both agents; they must be current before the next
+// rollout's commit), 2 << a = agent a's learner results and schedules (after its BR chain)
 template <int TABLE>   // TABLE: engine groups, block = replica of `tab`
-__global__ void k_finalize(FinalArgs F0, const FinalArgs* __restrict__ tab) {
+__global__ void k_finalize(FinalArgs F0, const FinalArgs* __restrict__ tab, int mode) {
   const FinalArgs& F = TABLE ? tab[blockIdx.x] : F0;
   if (threadIdx.x != 0) return;
   for (int a = 0; a < 2; ++a) {
     EngineDev* st = F.st;
-    st->rl_total[a] += F.n_rl[a];
-    st->sl_total[a] += F.n_sl[a];
-    st->sl_count[a] = st->sl_total[a] < F.sl_cap ? st->sl_total[a] : F.sl_cap;
-    if (F.U_br[a] > 0) {
+    if (mode & 1) {
+      st->rl_total[a] += F.n_rl[a];
+      st->sl_total[a] += F.n_sl[a];
+      st->sl_count[a] = st->sl_total[a] < F.sl_cap ? st->sl_total[a] : F.sl_cap;
+    }
+    if ((mode & (2 << a)) && F.U_br[a] > 0) {
       st->expl[a] = F.br_expl[(int64_t)a * F.umax + F.U_br[a] - 1];
       st->br_updates[a] += F.U_br[a];
       st->iteration[a] = F.iteration[a];
@@ -519,8 +523,10 @@ int plan_update(nfsp_engine* e, const EngineDev& h, LearnPlan& L) {
     F.n_rl[a] = h.last_rl[a];
     F.n_sl[a] = pl.n_sl;
     F.U_br[a] = pl.U_br;
-    int64_t it = h.iteration[a], tc = h.target_count[a], syncs = h.target_syncs[a];
-    double eps = h.epsilon[a];
+    // the schedules from the host's mirror (the device copy in EngineDev, written by
+    // k_finalize, may still be in flight with cfg.slice_lag 2)
+    int64_t it = e->hs.iteration[a], tc = e->hs.target_count[a], syncs = e->hs.target_syncs[a];
+    double eps = e->hs.epsilon[a];
     L.it0[a] = it;
     // BR segments between target syncs: [u, v) ends after the first update whose
     // target_count % every == 0 (agent/agent.py:266-273)
@@ -555,6 +561,10 @@ int plan_update(nfsp_engine* e, const EngineDev& h, LearnPlan& L) {
     F.tcount[a] = tc;
     F.syncs[a] = syncs;
     F.eps[a] = eps;
+    e->hs.iteration[a] = it;
+    e->hs.target_count[a] = tc;
+    e->hs.target_syncs[a] = syncs;
+    e->hs.epsilon[a] = eps;
     F.temp[a] = 1.0 / (1.0 + 0.02 * sqrt((double)it));
     F.lr[a] = (float)(cfg.lr_br / (1.0 + 0.003 * sqrt((double)it)));
   }
@@ -651,11 +661,13 @@ int launch_br_chain(const ChainArgs& C, int blocks, unsigned quirks, bool loss_l
 
 }  // namespace
 
-extern "C" int nfsp_engine_update(nfsp_engine* e) {
-  NFSP_REQUIRE(e, "null argument");
-  NFSP_REQUIRE(e->s_ar, "a replica of an engine group is stepped by nfsp_group_step");
+// One learner call for the pending rollout.  par: the learner-buffer set (slice parity; 0
+// unless cfg.slice_lag 2).  pipelined: leave the chains running (no join into the ctx
+// stream; each BR stream publishes its agent's results itself), and when snap_after, copy
+// the nets into snapshot `par` after the chains and record snap_ev[par] for the rollout two
+// slices on (step_pipelined).
+static int update_impl(nfsp_engine* e, bool pipelined, int par, bool snap_after) {
   if (!e->pending_update) return NFSP_OK;
-  e->pending_update = false;
   hipStream_t s = e->ctx->stream;
   const nfsp_engine_cfg& cfg = e->cfg;
   // the trigger plan needs the rollout's insert counts: one small readback
@@ -663,9 +675,13 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
   NFSP_HIP(hipMemcpyAsync(&h, e->st, sizeof(h), hipMemcpyDeviceToHost, s));
   NFSP_HIP(hipStreamSynchronize(s));
   KTimer kt(e, KT_LEARNER);
+  e->LB = e->LBs[par];
   LearnPlan L;
   int rc = plan_update(e, h, L);
   if (rc != NFSP_OK) return rc;
+  e->pending_update = false;
+  if (pipelined)                       // the rollout two slices on acts with this epsilon
+    for (int a = 0; a < 2; ++a) e->snap_eps[par][a] = e->hs.epsilon[a];
   // ---- parallel prep on the ctx stream, in the order the chains need it: the BR rows
   // first (agent 0's BR segments are the learner's critical path), the BR streams fork;
   // then the AR records, the AR stream forks; the final reservoir last (only the next
@@ -679,15 +695,26 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
     NFSP_HIP(hipEventRecord(fork, s));
     if ((rc = launch_res_apply(L, s)) != NFSP_OK) return rc;
   }
+  if (pipelined) {                     // the counters, before the next rollout's commit
+    k_finalize<0><<<1, 64, 0, s>>>(L.F, nullptr, 1);
+    NFSP_LAUNCHED("k_finalize");
+  }
+  float* snap = e->snap + (size_t)par * 6 * nn::NP;
   // ---- AR chains (both agents, one launch) on their own stream
+  NFSP_HIP(hipStreamWaitEvent(e->s_ar, fork, 0));
   if (L.maxU > 0) {
-    NFSP_HIP(hipStreamWaitEvent(e->s_ar, fork, 0));
     ChainArgs C{};
     C.B = cfg.batch;
     C.E = cfg.epochs;
     for (int a = 0; a < 2; ++a) C.job[a] = ar_job(e, L, a);
     KTimer kc(e, KT_CHAIN_AR, e->s_ar);
     if ((rc = launch_chain_ar(C, 2, e->log_loss, e->s_ar)) != NFSP_OK) return rc;
+  }
+  if (snap_after) {
+    for (int a = 0; a < 2; ++a)
+      NFSP_HIP(hipMemcpyAsync(snap + (a * 3 + 0) * nn::NP, e->w + (a * 3 + 0) * nn::NP,
+                              sizeof(float) * nn::NP, hipMemcpyDeviceToDevice, e->s_ar));
+    NFSP_HIP(hipEventRecord(e->snap_ev[par][0], e->s_ar));
   }
   // diagnostic (NFSP_LEARNER_SERIAL=1): BR work waits for the AR chains, to time them alone
   static const bool serial_ar = getenv("NFSP_LEARNER_SERIAL") && atoi(getenv("NFSP_LEARNER_SERIAL"));
@@ -716,7 +743,20 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
       KTimer kc(e, KT_CHAIN_BR, sa);
       if ((rc = launch_br_chain(C, 1, cfg.quirks, e->log_loss, sa)) != NFSP_OK) return rc;
     }
+    if (pipelined) {                   // this agent's learner results, after its chain
+      k_finalize<0><<<1, 64, 0, sa>>>(L.F, nullptr, 2 << a);
+      NFSP_LAUNCHED("k_finalize");
+    }
+    if (snap_after) {
+      NFSP_HIP(hipMemcpyAsync(snap + (a * 3 + 1) * nn::NP, e->w + (a * 3 + 1) * nn::NP,
+                              sizeof(float) * nn::NP, hipMemcpyDeviceToDevice, sa));
+      NFSP_HIP(hipEventRecord(e->snap_ev[par][1 + a], sa));
+    }
   }
+  e->pool.push_back(fork);
+  e->pool.push_back(fork_br);
+  if (ar_done != fork) e->pool.push_back(ar_done);
+  if (pipelined) return NFSP_OK;
   // ---- join and publish the schedules
   for (hipStream_t st : {e->s_ar, e->s_br[0], e->s_br[1]}) {
     hipEvent_t j = take_event(e);
@@ -724,13 +764,58 @@ extern "C" int nfsp_engine_update(nfsp_engine* e) {
     NFSP_HIP(hipStreamWaitEvent(s, j, 0));
     e->pool.push_back(j);      // reusable once the wait is enqueued
   }
-  e->pool.push_back(fork);
-  e->pool.push_back(fork_br);
-  if (ar_done != fork) e->pool.push_back(ar_done);
-  k_finalize<0><<<1, 64, 0, s>>>(L.F, nullptr);
+  k_finalize<0><<<1, 64, 0, s>>>(L.F, nullptr, 7);
   NFSP_LAUNCHED("k_finalize");
   return NFSP_OK;
 }
+
+// the side streams' work so far, joined into the ctx stream
+static int join_streams(nfsp_engine* e) {
+  for (hipStream_t st : {e->s_ar, e->s_br[0], e->s_br[1]}) {
+    hipEvent_t j = take_event(e);
+    NFSP_HIP(hipEventRecord(j, st));
+    NFSP_HIP(hipStreamWaitEvent(e->ctx->stream, j, 0));
+    e->pool.push_back(j);
+  }
+  return NFSP_OK;
+}
+
+extern "C" int nfsp_engine_update(nfsp_engine* e) {
+  NFSP_REQUIRE(e, "null argument");
+  NFSP_REQUIRE(e->s_ar, "a replica of an engine group is stepped by nfsp_group_step");
+  return update_impl(e, false, 0, false);
+}
+
+namespace nfsp {
+namespace eng {
+// nfsp_engine_step with cfg.slice_lag 2.  Slice j's rollout acts with snapshot j & 1: the
+// nets as of the step's start for j < 2, else as the chains of slice j - 2 left them (copied
+// on each chain stream right after its chain, so slice j - 1's chains may already run).  The
+// ctx stream waits only for those copies, never for the running chains: rollout, readback,
+// plan and prep of slice j overlap slice j - 1's chains, which the chain streams follow
+// without a gap.  The step ends with every stream joined (stats, weights and the next step
+// see all of it).
+int step_pipelined(nfsp_engine* e) {
+  hipStream_t s = e->ctx->stream;
+  const int K = e->slices;
+  for (int p = 0; p < 2; ++p) {
+    NFSP_HIP(hipMemcpyAsync(e->snap + (size_t)p * 6 * nn::NP, e->w, sizeof(float) * 6 * nn::NP,
+                            hipMemcpyDeviceToDevice, s));
+    for (int a = 0; a < 2; ++a) e->snap_eps[p][a] = e->hs.epsilon[a];
+  }
+  int rc;
+  for (int j = 0; j < K; ++j) {
+    const int par = j & 1;
+    if (j >= 2)
+      for (hipEvent_t ev : e->snap_ev[par]) NFSP_HIP(hipStreamWaitEvent(s, ev, 0));
+    if ((rc = rollout_launch_with(e, e->snap + (size_t)par * 6 * nn::NP, e->snap_eps[par])) != NFSP_OK)
+      return rc;
+    if ((rc = update_impl(e, true, par, j + 2 < K)) != NFSP_OK) return rc;
+  }
+  return join_streams(e);
+}
+}  // namespace eng
+}  // namespace nfsp
 
 // ---------------------------------------------------------------------------
 // Engine groups (nfsp_group_*): R replicas stepped together, their chains in shared launches
@@ -1039,8 +1124,17 @@ static int group_update(nfsp_group* g) {
   }
   e0->pool.push_back(fork);
   e0->pool.push_back(fork_br);
-  k_finalize<1><<<R, 64, 0, s>>>(FinalArgs{}, d_fin);
+  k_finalize<1><<<R, 64, 0, s>>>(FinalArgs{}, d_fin, 7);
   NFSP_LAUNCHED("k_finalize");
+  return NFSP_OK;
+}
+
+extern "C" int nfsp_engine_snapshot(nfsp_engine* e, int parity, float** dev_w, double* eps) {
+  NFSP_REQUIRE(e && dev_w && eps && (parity == 0 || parity == 1), "bad argument");
+  NFSP_REQUIRE(e->snap, "the engine has no snapshots (cfg.slice_lag 1)");
+  *dev_w = e->snap + (size_t)parity * 6 * nn::NP;
+  eps[0] = e->snap_eps[parity][0];
+  eps[1] = e->snap_eps[parity][1];
   return NFSP_OK;
 }
 

@@ -182,6 +182,17 @@ class SelfPlayEngine:
         c = c.astype(np.int64) & 0xFFFF
         return np.stack([(c >> (4 * k)) & 15 for k in range(4)], axis=1)
 
+    def snapshot(self, parity: int):
+        """(acting nets [2][3][NP] flat, (eps0, eps1)) of snapshot `parity` (cfg.slice_lag 2,
+        nfsp_engine_snapshot): after a pipelined step of K slices, parity (K - 1) & 1 is what
+        the last slice acted with."""
+        p = native.P()
+        eps = (C.c_double * 2)()
+        native.check(self.L.nfsp_engine_snapshot(self.h, int(parity), C.byref(p), eps), "snapshot")
+        torch.cuda.synchronize(self.dev)
+        w = _wrap_device(p.value, 6 * NP, torch.float32, self.dev, self).cpu().numpy().copy()
+        return w, (eps[0], eps[1])
+
     def set_update_limit(self, max_updates: int):
         """Test hook (nfsp_engine_set_update_limit): the chains run only a prefix of each
         learner call's updates."""

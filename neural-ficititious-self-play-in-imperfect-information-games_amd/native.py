@@ -39,7 +39,8 @@ class EngineCfg(C.Structure):
                 ("sl_capacity", I64), ("batch", C.c_int32), ("inserts_per_update", C.c_int32),
                 ("target_every", C.c_int32), ("epochs", C.c_int32), ("fit_batch", C.c_int32),
                 ("quirks", C.c_uint32), ("eta", F32), ("lr_br", F32), ("lr_ar", F32),
-                ("gamma", F64), ("epsilon", F64), ("seed", U64), ("slices", C.c_int32)]
+                ("gamma", F64), ("epsilon", F64), ("seed", U64), ("slices", C.c_int32),
+                ("slice_lag", C.c_int32)]
 
 
 class EngineStats(C.Structure):
@@ -109,6 +110,7 @@ SIGNATURES = {
     "nfsp_engine_set_timing": (I32, [P, I32]),
     "nfsp_engine_get_timings": (I32, [P, C.POINTER(F64), C.POINTER(I64)]),
     "nfsp_engine_set_update_limit": (I32, [P, I64]),
+    "nfsp_engine_snapshot": (I32, [P, I32, PP, P]),
     "nfsp_group_create": (I32, [P, C.POINTER(EngineCfg), I32, U32, C.POINTER(P)]),
     "nfsp_group_destroy": (I32, [P]),
     "nfsp_group_engine": (I32, [P, I32, C.POINTER(P)]),

@@ -132,11 +132,36 @@ def test_group_sharing_cus_matches_standalone_engines(pkg, R):
             e.step()
         torch.cuda.synchronize()
         for r in picks:
-            assert g.replicas[r].stats()["br_updates"] == solo[r].stats()["br_updates"], (step, r)
+            gs, ss = g.replicas[r].stats(), solo[r].stats()
+            for k in STAT_KEYS + ("rollouts",):      # incl. the counters past replica 64
+                assert gs[k] == ss[k], (step, r, k)
             for x, y in zip(nets(g.replicas[r]), nets(solo[r])):
                 assert np.array_equal(x, y), (step, r)
-    assert sum(g.stats()["br_updates"]) > 0
+    st = g.stats()
+    assert sum(st["br_updates"]) > 0
+    assert st["hands"] == 2 * R * kw["n_lanes"] and st["rollouts"] == 2 * R
     g.close()
+
+
+def test_sliced_group_matches_sliced_standalone_engines(pkg):
+    """cfg.slices in a group: every replica advances its lanes slice by slice like a sliced
+    standalone engine with its seed (the AR exchange after each whole step)."""
+    kw = dict(n_lanes=1024, slices=4, rl_capacity=3000, sl_capacity=2000, target_every=11)
+    R = 3
+    g = pkg.engine.EngineGroup(R, seed=555, init_seed=1, **kw)
+    solo = [pkg.engine.SelfPlayEngine(seed=555 + r, init_seed=1 + r, **kw) for r in range(R)]
+    for step in range(3):
+        g.step()
+        for e in solo:
+            e.step()
+        for r in range(R):
+            gs, ss = g.replicas[r].stats(), solo[r].stats()
+            for k in STAT_KEYS + ("rollouts",):
+                assert gs[k] == ss[k], (step, r, k)
+            for x, y in zip(nets(g.replicas[r]), nets(solo[r])):
+                assert np.array_equal(x, y), (step, r)
+    assert g.stats()["rollouts"] == 3 * 4 * R
+    assert min(g.stats()["br_updates"]) > 0
 
 
 def test_group_replica_count_bounds(pkg):

@@ -64,8 +64,9 @@ def test_slicing_leaves_every_hand_unchanged(pkg):
         assert np.array_equal(xa["sl_a"][:n].cpu().numpy(), xb["sl_a"][:n].cpu().numpy())
 
 
-def _check_slice_lanes(eng, seed, lanes, rl_before):
-    """Sampled local lanes of the last rollout vs the oracle's replay of their global lanes."""
+def _check_slice_lanes(eng, seed, lanes, rl_before, w=None, eps=None):
+    """Sampled local lanes of the last rollout vs the oracle's replay of their global lanes
+    (acting nets / epsilon: the engine's current ones unless given)."""
     lane0, g = eng.last_slice()
     st = eng.stats()
     cnt = eng.lane_counts()
@@ -73,8 +74,8 @@ def _check_slice_lanes(eng, seed, lanes, rl_before):
     assert cnt[:, 0].sum() == st["last_rl"][0] and cnt[:, 1].sum() == st["last_rl"][1]
     pre = np.zeros_like(cnt)
     pre[1:] = np.cumsum(cnt, axis=0)[:-1]
-    w = _weights_flat(eng)
-    eps = (float(st["epsilon"][0]), float(st["epsilon"][1]))
+    w = _weights_flat(eng) if w is None else w
+    eps = (float(st["epsilon"][0]), float(st["epsilon"][1])) if eps is None else eps
     mems = [eng.memories(p) for p in (0, 1)]
     for L in lanes:
         ref = R._one_lane(lane0 + L, g, seed, w, eps, eng.cfg.eta, True)
@@ -116,6 +117,47 @@ def test_c3_sliced_rollouts_replay_on_the_oracle(pkg):
         assert eng.last_slice() == (k * S, 1)
         _check_slice_lanes(eng, seed, _sample_lanes(S, 48, 10 + k), before)
         eng.update()
+
+
+@pytest.mark.parametrize("K", [2, 8])
+def test_pipelined_slices_act_with_the_nets_two_slices_back(pkg, K):
+    """cfg.slice_lag 2: slice j acts with the nets and epsilon left by slice j - 2's learner
+    (the step's start for j < 2), while slice j - 1's chains run.  The last slice of a step is
+    replayed on the oracle with exactly those nets: for K = 2 the nets from before the step,
+    for K = 8 the snapshot the engine kept (nfsp_engine_snapshot)."""
+    seed = 1357
+    eng = pkg.engine.SelfPlayEngine(seed=seed, init_seed=5, slices=K, slice_lag=2,
+                                    n_lanes=262_144, rl_capacity=200_000, sl_capacity=2_000_000)
+    eng.step()                                     # the learner has trained
+    w_start = _weights_flat(eng)
+    eps_start = tuple(float(v) for v in eng.stats()["epsilon"])
+    eng.step()
+    st = eng.stats()
+    assert st["rollouts"] == 2 * K and st["hands"] == 2 * 262_144
+    assert min(st["br_updates"]) > 100
+    if K == 2:
+        w, eps = w_start, eps_start
+    else:
+        w, eps = eng.snapshot((K - 1) & 1)
+        assert not np.array_equal(w, w_start)      # trained past the step's start
+    # the acting nets are not the final ones: the last slices' learners ran after they acted
+    assert not np.array_equal(w.reshape(2, 3, -1)[:, :2], _weights_flat(eng).reshape(2, 3, -1)[:, :2])
+    assert eng.last_slice() == ((K - 1) * eng.slice_lanes, 1)
+    before = tuple(int(st["rl_total"][p] - st["last_rl"][p]) for p in (0, 1))
+    _check_slice_lanes(eng, seed, _sample_lanes(eng.slice_lanes, 48, 20 + K), before, w, eps)
+
+
+def test_pipelined_step_is_deterministic(pkg):
+    def run():
+        e = pkg.engine.SelfPlayEngine(seed=808, init_seed=6, slices=16, slice_lag=2, **C3)
+        e.step()
+        e.step()
+        return e.stats(), _weights_flat(e)
+    s1, w1 = run()
+    torch.cuda.empty_cache()
+    s2, w2 = run()
+    assert s1 == s2
+    assert np.array_equal(w1, w2)
 
 
 def _band():
