@@ -52,13 +52,14 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 CONFIGS = {
-    # C3 advances its 1M lanes in 16 slices of 65,536, the learner consuming each slice's
-    # inserts before the next acts (include/nfsp.h cfg.slices): the policy lag is one slice,
-    # and C3 learns inside the CPU reference's seed band (tests/test_gpu_slices.py)
-    "c3": dict(n_lanes=1_048_576, slices=16, rl_capacity=200_000, sl_capacity=2_000_000,
-               label="C3: 1,048,576 Leduc lanes/GPU (advanced in 16 slices of 65,536), device M_RL 200k "
-                     "+ M_SL 2M, target sync 150, reference update cadence (1 update_strategy / 128 RL "
-                     "inserts / agent)"),
+    # C3 advances its 1M lanes in 16 slices of 65,536 (include/nfsp.h cfg.slices), pipelined
+    # (cfg.slice_lag 2: a slice acts with the nets its predecessor's predecessor's learner left,
+    # while its predecessor's chains run): the policy lag is 2 slices, not 1M hands, and C3
+    # learns inside the CPU reference's seed band (tests/test_gpu_slices.py)
+    "c3": dict(n_lanes=1_048_576, slices=16, slice_lag=2, rl_capacity=200_000, sl_capacity=2_000_000,
+               label="C3: 1,048,576 Leduc lanes/GPU (advanced in 16 pipelined slices of 65,536), device "
+                     "M_RL 200k + M_SL 2M, target sync 150, reference update cadence (1 update_strategy "
+                     "/ 128 RL inserts / agent)"),
     "c3_1slice": dict(n_lanes=1_048_576, rl_capacity=200_000, sl_capacity=2_000_000,
                       label="C3 with all 1,048,576 lanes in one rollout per step (round 2's form: policy "
                             "lag of 1M hands), M_RL 200k + M_SL 2M, reference cadence"),
@@ -316,7 +317,10 @@ def stub_main(args, world, rank, dist):
 def measure_group(pkg, name: str, steps: int, warmup: int) -> dict:
     """A side measurement beside the headline (N = 1): engine-group config `name` (C3's
     per-GPU lanes as R learner replicas, on-device AR exchange), W warmup + K un-instrumented
-    steps with the same sync protocol, and the exact exploitability after them."""
+    steps with the same sync protocol, and the exact exploitability after them.  The primary
+    figure is RL inserts/s: the learner's work follows the RL inserts (one update per 128),
+    and the inserts per hand grow as training goes on, so hands/s alone depends on the stage.
+    The stage is stated: the warmup is the headline's (W steps of 1,048,576 hands)."""
     import torch
     cfg = CONFIGS[name]
     R = cfg["replicas"]
@@ -331,7 +335,10 @@ def measure_group(pkg, name: str, steps: int, warmup: int) -> dict:
     hands = steps * cfg["n_lanes"]
     rl = sum(s1["rl_total"]) - sum(s0["rl_total"])
     out = {"workload": cfg["label"], "learner_replicas": R, "lanes_per_replica": cfg["n_lanes"] // R,
-           "value": hands / el, "unit": "hands/s", "steps": steps, "warmup": warmup,
+           "metric": "RL inserts/s (M_RL inserts, each 1/128 of an update_strategy)",
+           "value": rl / el, "unit": "inserts/s", "hands_per_s": hands / el,
+           "training_stage": {"warmup_steps": warmup, "hands_before_timing": warmup * cfg["n_lanes"]},
+           "steps": steps, "warmup": warmup,
            "ms_per_step": el / steps * 1e3, "rl_inserts_per_s": rl / el,
            "rl_inserts_per_hand": rl / hands,
            "exploitability_exact_softmax": g.exploitability(0)["exploitability"],
@@ -576,7 +583,7 @@ def main():
         eng.close()
         del eng
         torch.cuda.empty_cache()
-        out["groups"] = {name: measure_group(pkg, name, max(args.steps, 10), max(args.warmup, 2))
+        out["groups"] = {name: measure_group(pkg, name, max(args.steps, 10), args.warmup)
                          for name in args.groups.split(",")}
     if rank == 0 and world == 1 and not args.no_cpu:
         threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))

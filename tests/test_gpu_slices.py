@@ -166,15 +166,23 @@ def _band():
 
 
 def test_c3_sliced_learns_within_the_cpu_seed_band(pkg):
-    """BASELINE.json's second metric at C3: the exploitability-vs-hands curve of the 1M-lane
-    engine (16 slices) lies within the CPU reference's seed band."""
+    """BASELINE.json's second metric at C3, as bench.py measures C3 (1M lanes, 16 pipelined
+    slices): the exploitability-vs-hands curve lies within the CPU reference's seed band.
+    Bar at every checkpoint: |GPU mean - CPU mean| <= 2 sigma and GPU mean <= CPU mean + 1 sigma
+    (sigma: the 8 CPU seeds' std, ~0.25 chips; the GPU mean's own standard error is ~0.09).
+    Unsliced (one rollout of 1M hands per step) sat 1.1 sigma above the band
+    (profiles/r01_exploit_lag.json)."""
+    import bench
+    c3 = bench.CONFIGS["c3"]
+    K, lag = c3["slices"], c3["slice_lag"]
+    assert (K, lag) == (16, 2) and c3["n_lanes"] == C3["n_lanes"]
     band = _band()
     cpu = {int(h): np.array(v) for h, v in band["curves_by_hands"].items()}
     seeds = band["seeds"]
     checkpoints = (8, 16, 24, 32)                  # engine steps of 1,048,576 hands
     gpu = {c: [] for c in checkpoints}
     for s in seeds:
-        eng = pkg.engine.SelfPlayEngine(seed=1234 + s, init_seed=s, slices=16, **C3)
+        eng = pkg.engine.SelfPlayEngine(seed=1234 + s, init_seed=s, slices=K, slice_lag=lag, **C3)
         for k in range(1, checkpoints[-1] + 1):
             eng.step()
             if k in gpu:
@@ -192,3 +200,4 @@ def test_c3_sliced_learns_within_the_cpu_seed_band(pkg):
     print("hands, cpu checkpoint, cpu mean, cpu std, gpu mean, gpu std:", report)
     for (h, near, cm, cs, gm, gs) in report:
         assert abs(gm - cm) <= 2 * cs, report
+        assert gm <= cm + cs, report
