@@ -117,11 +117,12 @@ static __device__ unsigned long long g_chain_stamps[8][4][10];
 // rows g > 0 of w2t, the lanes past a record quarter) write to sink rows nobody reads, so
 // the loop has no exec-mask branches.
 struct Chain3Smem {
-  float po[2][4][64][4];     // per-wave partial layer-2 outputs by sample (rows 32..63: sink),
+  float po[2][4][64][4];     // per-wave partial layer-2 outputs by sample (rows 0..31 used),
                              // double-buffered by step parity
   float dm[4][3][64];        // wave-private: dL/dz2 of the 32 samples, by output (32..63: sink)
-  float4 w2t[4][64];         // wave-private: W2[h][0..2] of the slice for Z1^T (lane l writes
-                             // row l; rows 0..15 are read)
+  float4 w2t[4][64];         // wave-private: W2[h][0..2] of the slice (rows 0..15: the layer-2
+                             // weights live here, each component written by the lanes owning it)
+  float b2s[4][4];           // wave-private: b2
   StepRec ring[4];           // step records t .. t + 2 (slot t & 3), a quarter per wave
   uint4 rec_sink[64];
 };
@@ -141,47 +142,82 @@ inline int chain_lds_shared(int per_cu) {
 }
 
 // exact three-term bf16 split of 8 f32 values, a pair at a time: per pair and level one
-// packed conversion (v_cvt_pk_bf16_f32, round to nearest even) and the two residuals by
-// v_dot2c_f32_bf16: a - hi(a) = dot((hi(a), hi(b)), (-1, 0)) + a, exact (the product is
-// exact and the difference is representable).  v = hi + mid + lo exactly.  That is 7
-// instructions per pair instead of 11 (a shift / mask and a subtract per residual):
-// BR 0.906 -> 0.884 us, AR 0.93 -> 0.923 us per SGD step, results bit-identical
-// (tools/chain_ab.sh).  Two details:
-//  * the (-1, 0) / (0, -1) operands come from VGPRs: written as the literal 0x0000bf80 the
-//    pair did not reach the instruction as given;
-//  * the conversions are plain C++ casts, so the compiler sees every consumer of the dot2c
-//    results: gfx950 needs wait states between a DOT instruction's write and another VALU
-//    instruction's read, which the compiler inserts only for instructions it knows.  With
-//    the conversion as inline asm the chain's results moved (up to 2e-3 after 200 updates),
-//    although each residual alone was exact
+// packed conversion (v_cvt_pk_bf16_f32, round to nearest even) and the two residuals by a
+// bf16 dot: a - hi(a) = dot((hi(a), hi(b)), (-1, 0)) + a, exact (the product is exact and the
+// difference is representable).  v = hi + mid + lo exactly.  7 instructions per pair instead
+// of 11 (a shift / mask and a subtract per residual).  History (tools/chain_ab.sh, results
+// bit-identical throughout): the builtin's accumulating v_dot2c_f32_bf16 took BR 0.906 ->
+// 0.884 us, AR 0.93 -> 0.923 us per SGD step; the asm form below saves its v_movs (0.885 ->
+// 0.877 / 0.930 -> 0.921).  Details:
+//  * the (-1, 0) / (0, -1) operands come from VGPRs made once per kernel: written as the
+//    literal 0x0000bf80 the pair did not reach the instruction as given;
+//  * an asm conversion next to compiler-placed dot2c moved the chain's results (up to 2e-3
+//    after 200 updates): gfx950 needs wait states between a DOT write and another VALU
+//    instruction's read, and the compiler pads only for instructions it can see.  So the
+//    whole split is ONE asm statement that spaces them itself.
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 __device__ inline uint32_t cvt_pk_bf16(float a, float b) {
   const bf16x2 r = {(__bf16)a, (__bf16)b};
   return __builtin_bit_cast(uint32_t, r);
 }
-__device__ inline void split3(const float (&v)[8], bf16x8& hi, bf16x8& mid, bf16x8& lo) {
-#pragma clang fp contract(off)
-  uint32_t h[4], m[4], o[4];
+// the (-1, 0) / (0, -1) bf16 pairs of the residual dots, made once per kernel
+struct SplitK {
   uint32_t cl, ch;
-  asm("v_mov_b32 %0, 0xbf80" : "=v"(cl));
-  asm("v_mov_b32 %0, 0xbf800000" : "=v"(ch));
-  const bf16x2 nlo = __builtin_bit_cast(bf16x2, cl), nhi = __builtin_bit_cast(bf16x2, ch);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const float a = v[2 * k], b = v[2 * k + 1];
-    h[k] = cvt_pk_bf16(a, b);
-    const bf16x2 hv = __builtin_bit_cast(bf16x2, h[k]);
-    const float ra = __builtin_amdgcn_fdot2_f32_bf16(hv, nlo, a, false);
-    const float rb = __builtin_amdgcn_fdot2_f32_bf16(hv, nhi, b, false);
-    m[k] = cvt_pk_bf16(ra, rb);
-    const bf16x2 mv = __builtin_bit_cast(bf16x2, m[k]);
-    const float sa = __builtin_amdgcn_fdot2_f32_bf16(mv, nlo, ra, false);
-    const float sb = __builtin_amdgcn_fdot2_f32_bf16(mv, nhi, rb, false);
-    o[k] = cvt_pk_bf16(sa, sb);
-  }
-  hi = __builtin_bit_cast(bf16x8, make_uint4(h[0], h[1], h[2], h[3]));
-  mid = __builtin_bit_cast(bf16x8, make_uint4(m[0], m[1], m[2], m[3]));
-  lo = __builtin_bit_cast(bf16x8, make_uint4(o[0], o[1], o[2], o[3]));
+};
+__device__ inline SplitK split_consts() {
+  SplitK k;
+  asm volatile("v_mov_b32 %0, 0xbf80" : "=v"(k.cl));
+  asm volatile("v_mov_b32 %0, 0xbf800000" : "=v"(k.ch));
+  return k;
+}
+// The whole split in one asm statement with the non-destructive VOP3P v_dot2_f32_bf16 (the
+// builtin selects the accumulating v_dot2c_f32_bf16, so each residual of a value that stays
+// live -- the weights -- costs a v_mov first).  Wait states, all inside the string: a DOT
+// result is read by another VALU instruction only >= 4 instructions later (the gfx950 rule is
+// 3); the residual dots read the previous level's residual as their accumulator (SrcC); the
+// string ends with s_nop 1 for the MFMAs that read hi / mid / lo as operands.
+__device__ inline void split3(const float (&v)[8], bf16x8& hi, bf16x8& mid, bf16x8& lo, SplitK K) {
+  uint32_t h0, h1, h2, h3, m0, m1, m2, m3, o0, o1, o2, o3;
+  float r0, r1, r2, r3, r4, r5, r6, r7;
+  asm volatile(
+      "v_cvt_pk_bf16_f32 %0, %20, %21\n\t"
+      "v_cvt_pk_bf16_f32 %1, %22, %23\n\t"
+      "v_cvt_pk_bf16_f32 %2, %24, %25\n\t"
+      "v_cvt_pk_bf16_f32 %3, %26, %27\n\t"
+      "v_dot2_f32_bf16 %12, %0, %28, %20\n\t"
+      "v_dot2_f32_bf16 %13, %0, %29, %21\n\t"
+      "v_dot2_f32_bf16 %14, %1, %28, %22\n\t"
+      "v_dot2_f32_bf16 %15, %1, %29, %23\n\t"
+      "v_dot2_f32_bf16 %16, %2, %28, %24\n\t"
+      "v_dot2_f32_bf16 %17, %2, %29, %25\n\t"
+      "v_dot2_f32_bf16 %18, %3, %28, %26\n\t"
+      "v_dot2_f32_bf16 %19, %3, %29, %27\n\t"
+      "v_cvt_pk_bf16_f32 %4, %12, %13\n\t"
+      "v_cvt_pk_bf16_f32 %5, %14, %15\n\t"
+      "v_cvt_pk_bf16_f32 %6, %16, %17\n\t"
+      "v_dot2_f32_bf16 %12, %4, %28, %12\n\t"
+      "v_dot2_f32_bf16 %13, %4, %29, %13\n\t"
+      "v_cvt_pk_bf16_f32 %7, %18, %19\n\t"
+      "v_dot2_f32_bf16 %14, %5, %28, %14\n\t"
+      "v_dot2_f32_bf16 %15, %5, %29, %15\n\t"
+      "v_dot2_f32_bf16 %16, %6, %28, %16\n\t"
+      "v_dot2_f32_bf16 %17, %6, %29, %17\n\t"
+      "v_dot2_f32_bf16 %18, %7, %28, %18\n\t"
+      "v_dot2_f32_bf16 %19, %7, %29, %19\n\t"
+      "v_cvt_pk_bf16_f32 %8, %12, %13\n\t"
+      "v_cvt_pk_bf16_f32 %9, %14, %15\n\t"
+      "v_cvt_pk_bf16_f32 %10, %16, %17\n\t"
+      "s_nop 0\n\t"
+      "v_cvt_pk_bf16_f32 %11, %18, %19\n\t"
+      "s_nop 1"
+      : "=&v"(h0), "=&v"(h1), "=&v"(h2), "=&v"(h3), "=&v"(m0), "=&v"(m1), "=&v"(m2), "=&v"(m3),
+        "=&v"(o0), "=&v"(o1), "=&v"(o2), "=&v"(o3), "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3),
+        "=&v"(r4), "=&v"(r5), "=&v"(r6), "=&v"(r7)
+      : "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]),
+        "v"(K.cl), "v"(K.ch));
+  hi = __builtin_bit_cast(bf16x8, make_uint4(h0, h1, h2, h3));
+  mid = __builtin_bit_cast(bf16x8, make_uint4(m0, m1, m2, m3));
+  lo = __builtin_bit_cast(bf16x8, make_uint4(o0, o1, o2, o3));
 }
 
 __device__ inline floatx4 mfma3(bf16x8 a, bf16x8 bhi, bf16x8 bmid, bf16x8 blo) {
@@ -259,6 +295,14 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
     sm.w2t[w][l] = make_float4(W2_0, W2_1, W2_2, 0.f);
   };
   const int prow = 32 * (g & 1) + sl;          // po / dm row: the sample, or the sink
+  const SplitK SK = split_consts();
+  // W2 and b2 live in the wave's LDS (w2t rows 0..15, b2s); the cross-lane reductions leave
+  // each gradient total in one row of lanes (see the update), and that row owns the value:
+  //   row 0: W2[c][0]   row 1: W2[c][2]   row 2: W2[c][1]   row 3: b2[0]  (own1; row 3's total
+  //   is 2 gb2[0], scaled by 1/2 -- exact)        rows 0, 1: b2[1]   rows 2, 3: b2[2]  (own2)
+  float* const own1 = g == 3 ? &sm.b2s[w][0] : reinterpret_cast<float*>(&sm.w2t[w][c]) + (g == 0 ? 0 : g == 1 ? 2 : 1);
+  float* const own2 = &sm.b2s[w][g < 2 ? 1 : 2];
+  const float own1_sc = g == 3 ? 0.5f : 1.0f;
 #ifdef NFSP_CHAIN_STAMPS
   unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_last = 0;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
@@ -279,13 +323,17 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
     const bf16x8 ba1 = __builtin_bit_cast(bf16x8, R.ba[g][16 + c]);
     // ---- layer 1, both orientations
     bf16x8 whi, wmid, wlo;
-    split3(wr, whi, wmid, wlo);
+    split3(wr, whi, wmid, wlo, SK);
     float W2h[4][3];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float4 q = sm.w2t[w][4 * g + r];
       W2h[r][0] = q.x; W2h[r][1] = q.y; W2h[r][2] = q.z;
     }
+    const float4 w2c = sm.w2t[w][c];             // W2 of this lane's hidden unit (backward)
+    const float W2_0 = w2c.x, W2_1 = w2c.y, W2_2 = w2c.z;
+    const float4 b2v = *reinterpret_cast<const float4*>(&sm.b2s[w][0]);
+    const float b2_0 = b2v.x, b2_1 = b2v.y, b2_2 = b2v.z;
     // Z1^T first (layer 2 waits on it); Z1 (needed only by the backward) is issued after
     // layer 2, so its matrix-core time overlaps the barrier wait
     const floatx4 zh0 = mfma3t(whi, wmid, wlo, fa0);     // Z1^T: hidden 16w+4g+r, sample c
@@ -306,15 +354,21 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
         p1[k] = p1[k] + h1 * W2h[r][k];
       }
     }
+    const int buf = t & 1;
     float q[3];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {   // rows g, g ^ 2 (tile halves), then g ^ 1
+    for (int k = 0; k < 3; ++k) {   // rows g, g ^ 2 (tile halves)
       const auto rr = __builtin_amdgcn_permlane32_swap(__float_as_uint(p0[k]), __float_as_uint(p1[k]),
                                                        false, false);
-      q[k] = sum_x16(__uint_as_float(rr[0]) + __uint_as_float(rr[1]));
+      q[k] = __uint_as_float(rr[0]) + __uint_as_float(rr[1]);
     }
-    const int buf = t & 1;
-    *reinterpret_cast<float4*>(&sm.po[buf][w][prow][0]) = make_float4(q[0], q[1], q[2], 0.f);
+    {   // rows g, g ^ 1: outputs 0 and 1 in one swap (even rows get output 0's sum, odd rows
+        // output 1's), output 2 alone; every lane stores what it holds (same sums as before)
+      const auto r01 = __builtin_amdgcn_permlane16_swap(__float_as_uint(q[0]), __float_as_uint(q[1]), false, false);
+      float* const pr = &sm.po[buf][w][sl][0];
+      pr[g & 1] = __uint_as_float(r01[0]) + __uint_as_float(r01[1]);
+      pr[2] = sum_x16(q[2]);
+    }
     __builtin_amdgcn_sched_barrier(0);
     const floatx4 zs0 = mfma3(fa0, whi, wmid, wlo);      // Z1: sample 4g+r, hidden 16w+c
     const floatx4 zs1 = mfma3(fa1, whi, wmid, wlo);      //     sample 16+4g+r
@@ -419,7 +473,7 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
       x = x + dpp_any(x, 0x124);
       x = x + dpp_any(x, 0x122);
       x = x + dpp_any(x, 0x121);
-      gb2[k] = sum_x32(x);
+      gb2[k] = x;                    // the row's sum; rows g ^ 2 join in the update's swaps
     }
     CHAIN_STAMP(3);
     // ---- backward in the sample-major layout: samples 16 mt + 4g + r, hidden 16w + c
@@ -447,22 +501,33 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
       dz[j] = z > 0.f ? dh : 0.f;
     }
     bf16x8 dhi, dmid, dlo;
-    split3(dz, dhi, dmid, dlo);
+    split3(dz, dhi, dmid, dlo, SK);
     // dW1[16 it + 4g + r][16w + c] = sum over the 32 samples in dz's K order (row 30: gb1)
     const floatx4 gA = mfma3(ba0, dhi, dmid, dlo);
     const floatx4 gB = mfma3(ba1, dhi, dmid, dlo);
-    g2_0 = sum_x16(sum_x32(g2_0));
-    g2_1 = sum_x16(sum_x32(g2_1));
-    g2_2 = sum_x16(sum_x32(g2_2));
+    // The four row totals of (g2_0, g2_1, g2_2, gb2 row sums of output 0) in one transpose:
+    // two swaps across rows g ^ 2, one across g ^ 1 leave g2_0's total in row 0, g2_2's in row 1,
+    // g2_1's in row 2 and 2 gb2[0] in row 3 (rows 0 / 1 and 2 / 3 hold the same samples' sums),
+    // each added (r0 + r2) + (r1 + r3) as sum_x16(sum_x32(.)) did; gb2[1] / gb2[2] in one more
+    // swap, rows 0-1 / 2-3.  Each row updates the values it holds (own1, own2).
+    float V, U;
+    {
+      const auto ab = __builtin_amdgcn_permlane32_swap(__float_as_uint(g2_0), __float_as_uint(g2_1), false, false);
+      const float tab = __uint_as_float(ab[0]) + __uint_as_float(ab[1]);
+      const auto cd = __builtin_amdgcn_permlane32_swap(__float_as_uint(g2_2), __float_as_uint(gb2[0]), false, false);
+      const float tcd = __uint_as_float(cd[0]) + __uint_as_float(cd[1]);
+      const auto z = __builtin_amdgcn_permlane16_swap(__float_as_uint(tab), __float_as_uint(tcd), false, false);
+      V = __uint_as_float(z[0]) + __uint_as_float(z[1]);
+      const auto uu = __builtin_amdgcn_permlane32_swap(__float_as_uint(gb2[1]), __float_as_uint(gb2[2]), false, false);
+      U = __uint_as_float(uu[0]) + __uint_as_float(uu[1]);
+    }
     CHAIN_STAMP(4);
     const float lr = lr_step;
-    W2_0 = W2_0 - lr * g2_0;
-    W2_1 = W2_1 - lr * g2_1;
-    W2_2 = W2_2 - lr * g2_2;
-    b2_0 = b2_0 - lr * gb2[0];
-    b2_1 = b2_1 - lr * gb2[1];
-    b2_2 = b2_2 - lr * gb2[2];
-    publish();
+    {
+      const float v1 = *own1, v2 = *own2;
+      *own1 = v1 - (lr * own1_sc) * V;
+      *own2 = v2 - lr * U;
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       wr[r] = wr[r] - lr * gA[r];
@@ -480,6 +545,7 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
       stash(t + 1, va, vb);
     }
     publish();
+    if (l < 3) sm.b2s[w][l] = l == 0 ? b2_0 : l == 1 ? b2_1 : b2_2;
     __syncthreads();
     // drain the prologue's loads: the loop header then merges no pending load into the
     // registers the loop reuses (else every step waits on its fresh record load)
@@ -500,6 +566,11 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
     }
   }
 #endif
+  if (t > (int)(u0 * spu)) {             // the loop ran: W2 / b2 as the last step left them
+    const float4 fw = sm.w2t[w][c];
+    W2_0 = fw.x; W2_1 = fw.y; W2_2 = fw.z;
+    b2_0 = sm.b2s[w][0]; b2_1 = sm.b2s[w][1]; b2_2 = sm.b2s[w][2];
+  }
   float* dsts[2] = {gw, J.sync_to};
   for (int k = 0; k < 2; ++k) {
     float* dst = dsts[k];

@@ -172,8 +172,10 @@ int main(int argc, char** argv) {
   std::vector<float> wout(nn::NP);
   CK(hipMemcpy(wout.data(), dw, wout.size() * 4, hipMemcpyDeviceToHost));
   double cs = 0; for (float v : wout) cs += v;
-  printf("k_chain3 blocks=%d checksum=%.9g relu=%d updates=%d sgd_steps=%d  %.3f ms  %.3f us/step  %.2f us/update\n",
-         nblk, cs, relu, U, steps, ms, ms * 1e3 / steps, ms * 1e3 / U);
+  unsigned long long hsh = 1469598103934665603ull;     // FNV-1a over the weights' bits
+  for (float v : wout) { uint32_t u; memcpy(&u, &v, 4); hsh = (hsh ^ u) * 1099511628211ull; }
+  printf("k_chain3 blocks=%d checksum=%.9g hash=%016llx relu=%d updates=%d sgd_steps=%d  %.3f ms  %.3f us/step  %.2f us/update\n",
+         nblk, cs, hsh, relu, U, steps, ms, ms * 1e3 / steps, ms * 1e3 / U);
   std::vector<unsigned long long> st(80);
   CK(hipMemcpy(st.data(), dst, 80 * 8, hipMemcpyDeviceToHost));
   const char* names[6] = {"fwd-mfma", "layer2+po", "barrier", "loss+gb2", "bwd+dW1", "update+load"};

@@ -7,4 +7,4 @@ PKG=neural-ficititious-self-play-in-imperfect-information-games_amd
 F="--offload-arch=gfx950 -O3 -std=c++17 -mllvm -amdgpu-mfma-vgpr-form -fno-slp-vectorize -fno-honor-nans -falign-loops=64 -mllvm -amdgpu-sched-strategy=max-ilp -Iinclude -I$PKG/csrc"
 mkdir -p tools/bin
 hipcc $F "$@" tools/bench_chain.hip -o tools/bin/bench_chain_${tag}_ar
-hipcc $F -mllvm -amdgpu-use-amdgpu-trackers "$@" tools/bench_chain.hip -o tools/bin/bench_chain_${tag}_br
+hipcc $F "$@" tools/bench_chain.hip -o tools/bin/bench_chain_${tag}_br
