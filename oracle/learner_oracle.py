@@ -110,6 +110,52 @@ def bits_to_x(bits):
     return ((bits[:, None] >> np.arange(30)) & 1).astype(np.float32)
 
 
+def ar_minibatches(cfg, state, a, quirks=7, slots=None):
+    """The AR updates of agent a's learner call, in order: yields (u, bits [B], targets [B, 3],
+    perms [E, B]) -- M_SL as of the trigger (k_ar_prep) -- or (u, None, None, None) for an
+    update skipped because M_SL holds <= batch records.  The inputs of an AR update do not
+    depend on the weights, so any stretch of the chain can be replayed from given weights."""
+    c, B, E = cfg["c"], cfg["batch"], cfg["epochs"]
+    k0, k1 = cfg["seed"] & M32, (cfg["seed"] >> 32) & M32
+    st = state[a]
+    P0 = st["rl_total"] - st["last_rl"]
+    m_first = P0 // c + 1
+    m_last = (P0 + st["last_rl"]) // c
+    U = max(0, m_last - m_first + 1)
+    n_sl = st["last_sl"]
+    sl0 = st["sl_total"] - n_sl
+    cap = cfg["sl_capacity"]
+    if slots is None:
+        slots = reservoir_slots(a, sl0, n_sl, cap, k0, k1, quirks)
+    pos = np.asarray(st["pend_pos"][:n_sl], np.int64)
+    # each slot's inserts of this rollout in insert order: the latest one before a
+    # trigger is a bisection (slot contents as of the trigger)
+    order = np.argsort(slots, kind="stable")
+    ss = slots[order]
+    for u in range(U):
+        m = m_first + u
+        pm = m * c
+        nb = int(np.searchsorted(pos, pm, side="right"))
+        count = min(sl0 + nb, cap)
+        if count <= B:
+            yield u, None, None, None
+            continue
+        picks = sample_distinct(B, 0, count, TAG_SAMPLE | (a * 2), m, k0, k1)
+        xb = np.empty(B, np.int64)
+        ya = np.empty((B, 3), np.float32)
+        for b, j in enumerate(picks):
+            lo, hi = np.searchsorted(ss, j, side="left"), np.searchsorted(ss, j, side="right")
+            qs = order[lo:hi]                           # this slot's inserts, ascending
+            k = int(np.searchsorted(qs, nb, side="left"))
+            if k:
+                q = qs[k - 1]
+                xb[b], ya[b] = st["pend_x"][q], st["pend_a"][q]
+            else:
+                xb[b], ya[b] = st["sl_s_bits"][j], st["sl_a"][j]
+        perms = np.stack([draw_perm(B, e, TAG_PERM | (a * 2), m, k0, k1) for e in range(E)])
+        yield u, xb, ya, perms
+
+
 def learner_step(cfg, state, quirks=7, max_updates=None, trace=None):
     """Replay nfsp_engine_update.
 
@@ -182,35 +228,13 @@ def learner_step(cfg, state, quirks=7, max_updates=None, trace=None):
         sl0 = st["sl_total"] - n_sl
         cap = cfg["sl_capacity"]
         slots = reservoir_slots(a, sl0, n_sl, cap, k0, k1, quirks)
-        pos = np.asarray(st["pend_pos"][:n_sl], np.int64)
-        # each slot's inserts of this rollout in insert order: the latest one before a
-        # trigger is a bisection (slot contents as of the trigger)
-        order = np.argsort(slots, kind="stable")
-        ss = slots[order]
         n_ar = 0
-        for u in range(U):
-            m = m_first + u
-            pm = m * c
-            nb = int(np.searchsorted(pos, pm, side="right"))
-            count = min(sl0 + nb, cap)
-            if count <= B:
+        for u, xb, ya, perms in ar_minibatches(cfg, state, a, quirks, slots):
+            if xb is None:
                 continue
             n_ar += 1
             if u >= lim(U):
                 continue
-            picks = sample_distinct(B, 0, count, TAG_SAMPLE | (a * 2), m, k0, k1)
-            xb = np.empty(B, np.int64)
-            ya = np.empty((B, 3), np.float32)
-            for b, j in enumerate(picks):
-                lo, hi = np.searchsorted(ss, j, side="left"), np.searchsorted(ss, j, side="right")
-                qs = order[lo:hi]                           # this slot's inserts, ascending
-                k = int(np.searchsorted(qs, nb, side="left"))
-                if k:
-                    q = qs[k - 1]
-                    xb[b], ya[b] = st["pend_x"][q], st["pend_a"][q]
-                else:
-                    xb[b], ya[b] = st["sl_s_bits"][j], st["sl_a"][j]
-            perms = np.stack([draw_perm(B, e, TAG_PERM | (a * 2), m, k0, k1) for e in range(E)])
             ar.fit(bits_to_x(xb), ya, np.float32(cfg["lr_ar"]), epochs=E, perms=perms)
             if trace is not None:
                 trace(a, 0, u, ar.flat())

@@ -131,6 +131,8 @@ class MLP:
             # categorical_crossentropy, TF backend, from_logits=False.
             S = y.sum(axis=-1, keepdims=True)
             p = y / S
+            if getattr(self, "clip_probe", None) is not None:   # tests: where the clip mask sits
+                self.clip_probe(p)
             pc = np.clip(p, CE_EPS, F32(1.0) - CE_EPS)
             mask = ((p >= CE_EPS) & (p <= F32(1.0) - CE_EPS)).astype(F32)
             dldp = (-t2d / pc) * mask / F32(m)
@@ -140,6 +142,8 @@ class MLP:
         gW2 = h.T @ dz2
         gb2 = dz2.sum(axis=0)
         dh = dz2 @ self.W2.T
+        if getattr(self, "relu_probe", None) is not None:    # tests: how close a ReLU is to its kink
+            self.relu_probe(z1)
         dz1 = dh * (z1 > 0).astype(F32)
         gW1 = x2d.T @ dz1
         gb1 = dz1.sum(axis=0)
