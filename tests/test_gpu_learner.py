@@ -94,9 +94,10 @@ def test_learner_step_matches_oracle(pkg, case, quirks):
         assert st1["lr_br"][a] == pytest.approx(W["lr_br"], rel=1e-7)
         assert st1["temp"][a] == pytest.approx(W["temp"], rel=1e-12)
         assert st1["exploitability"][a] == pytest.approx(W["exploitability"], abs=1e-4)
-        # Under the textbook extensions (quirks >= 8) one-hot AR targets saturate the softmax,
-        # where Keras' clip mask at 1 - 1e-7 follows 1-ulp differences of exp, and the linear
-        # Q head moves more hidden units across zero: a single flipped decision in ~480 SGD
+        # Under the textbook extensions (quirks >= 8) the linear Q head moves more hidden units
+        # across zero, where a ReLU's derivative follows the summation order (the cause
+        # test_gpu_learner_divergence.py measures), and one-hot AR targets saturate the softmax
+        # (its clip mask is the other discrete decision): a single flipped decision in ~480 SGD
         # steps leaves a net up to ~2e-4 away (measured 1.2e-4 .. 3.3e-4) while the median
         # stays at ~1e-7.  Bars: 1e-3 / 1e-6 there; 1e-4 / 1e-7 for the reference.
         tol_max, tol_med = (1e-3, 1e-6) if quirks >= 8 else (1e-4, 1e-7)
