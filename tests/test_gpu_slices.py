@@ -12,7 +12,9 @@ update trigger agent/agent.py:153-154).
 * the C3 learning gate: exact exploitability after 8M / 16M / 25M / 33M hands at C3 (1M
   lanes, 16 slices, M_RL 200k, M_SL 2M) against the CPU seed band of the reference's
   main.train restated in C++ with the same memories and initial nets
-  (tests/golden/cpu_band_c3mem.json).
+  (tests/golden/cpu_band_c3mem.json);
+* the same gate for C4's arithmetic (8 x 1M lanes with the per-step average-policy
+  exchange), emulated on one GPU by an engine group.
 """
 import json
 import os
@@ -194,6 +196,48 @@ def test_c3_sliced_learns_within_the_cpu_seed_band(pkg):
     for k in checkpoints:
         h = k * C3["n_lanes"]
         near = min(cpu, key=lambda x: abs(x - h))  # the CPU checkpoint (every 2M hands) nearest
+        cm, cs = float(cpu[near].mean()), float(cpu[near].std())
+        gm, gs = float(np.mean(gpu[k])), float(np.std(gpu[k]))
+        report.append((h, near, round(cm, 3), round(cs, 3), round(gm, 3), round(gs, 3)))
+    print("hands, cpu checkpoint, cpu mean, cpu std, gpu mean, gpu std:", report)
+    for (h, near, cm, cs, gm, gs) in report:
+        assert abs(gm - cm) <= 2 * cs, report
+        assert gm <= cm + cs, report
+
+
+def test_c4_emulated_learns_within_the_cpu_seed_band(pkg):
+    """C4's arithmetic on one GPU: 8 shards of 1,048,576 lanes (C3's memories each, 16 slices),
+    the average-policy nets exchanged after every step (W0 + mean of the shards' deltas: the
+    RCCL exchange of bench.py --gpus 8, done on device by an engine group; the group runs its
+    slices with lag 1, the ranks' engines with lag 2).  Exploitability at equal TOTAL hands
+    against the CPU band.  Each step is 8.4M hands and one exchange, so the first steps learn
+    slower per hand than one learner; from 33.5M hands on (4 exchanges) the bar is the C3 one:
+    |GPU mean - CPU mean| <= 2 sigma and GPU mean <= CPU mean + 1 sigma.  Measured
+    (profiles/r03_exploit_c4_emulated_slices.json): 1.34 +- 0.12 at 33.5M, 1.19 +- 0.08 at 67M
+    against the CPU's 1.22 +- 0.24 at 32M; without slices (round 2) 1.68 +- 0.40 at 33M."""
+    band = _band()
+    cpu = {int(h): np.array(v) for h, v in band["curves_by_hands"].items()}
+    R, lanes = 8, 1_048_576
+    checkpoints = (4, 6, 8)                        # steps of 8 x 1,048,576 hands
+    gpu = {c: [] for c in checkpoints}
+    for s in range(4):
+        g = pkg.engine.EngineGroup(R, n_lanes=lanes, rl_capacity=C3["rl_capacity"],
+                                   sl_capacity=C3["sl_capacity"], seed=1234 + 1000 * s,
+                                   init_seed=1000 * s, avg_ar=True, slices=16)
+        g.average_ar()                             # the common start: replica 0's nets
+        for k in range(1, checkpoints[-1] + 1):
+            g.step()
+            if k in gpu:
+                gpu[k].append(g.exploitability(0)["exploitability"])
+        assert g.stats()["hands"] == checkpoints[-1] * R * lanes
+        g.close()
+        del g
+        torch.cuda.empty_cache()
+    report = []
+    last = max(cpu)
+    for k in checkpoints:
+        h = k * R * lanes
+        near = min(cpu, key=lambda x: abs(x - min(h, last)))
         cm, cs = float(cpu[near].mean()), float(cpu[near].std())
         gm, gs = float(np.mean(gpu[k])), float(np.std(gpu[k]))
         report.append((h, near, round(cm, 3), round(cs, 3), round(gm, 3), round(gs, 3)))
