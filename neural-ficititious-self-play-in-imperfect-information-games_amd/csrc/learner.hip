@@ -615,6 +615,7 @@ ChainJob ar_job(const nfsp_engine* e, const LearnPlan& L, int a) {
   ChainJob j{};
   j.w = e->w + (a * 3 + 0) * nn::NP;
   j.sync_to = nullptr;
+  j.snap_to = nullptr;
   j.rec = e->LB.ar_rec + a * um * recs_per_update(e);
   j.active = e->LB.ar_active + a * um;
   j.loss_out = e->log_loss ? e->LB.ar_loss + a * um * e->cfg.epochs : nullptr;
@@ -644,6 +645,7 @@ ChainJob br_chain_job(const nfsp_engine* e, int a, const Segment& sg) {
   ChainJob j{};
   j.w = e->w + (a * 3 + 1) * nn::NP;
   j.sync_to = sg.sync ? e->w + (a * 3 + 2) * nn::NP : nullptr;
+  j.snap_to = nullptr;
   j.rec = e->LB.br_rec + a * um * recs_per_update(e);
   j.active = nullptr;
   j.loss_out = e->log_loss ? e->LB.br_loss + a * um * e->cfg.epochs : nullptr;
@@ -706,16 +708,18 @@ static int update_impl(nfsp_engine* e, bool pipelined, int par, bool snap_after)
     ChainArgs C{};
     C.B = cfg.batch;
     C.E = cfg.epochs;
-    for (int a = 0; a < 2; ++a) C.job[a] = ar_job(e, L, a);
+    for (int a = 0; a < 2; ++a) {
+      C.job[a] = ar_job(e, L, a);
+      if (snap_after) C.job[a].snap_to = snap + (a * 3 + 0) * nn::NP;   // written by the chain
+    }
     KTimer kc(e, KT_CHAIN_AR, e->s_ar);
     if ((rc = launch_chain_ar(C, 2, e->log_loss, e->s_ar)) != NFSP_OK) return rc;
-  }
-  if (snap_after) {
+  } else if (snap_after) {
     for (int a = 0; a < 2; ++a)
       NFSP_HIP(hipMemcpyAsync(snap + (a * 3 + 0) * nn::NP, e->w + (a * 3 + 0) * nn::NP,
                               sizeof(float) * nn::NP, hipMemcpyDeviceToDevice, e->s_ar));
-    NFSP_HIP(hipEventRecord(e->snap_ev[par][0], e->s_ar));
   }
+  if (snap_after) NFSP_HIP(hipEventRecord(e->snap_ev[par][0], e->s_ar));
   // diagnostic (NFSP_LEARNER_SERIAL=1): BR work waits for the AR chains, to time them alone
   static const bool serial_ar = getenv("NFSP_LEARNER_SERIAL") && atoi(getenv("NFSP_LEARNER_SERIAL"));
   hipEvent_t ar_done = fork;
@@ -728,7 +732,8 @@ static int update_impl(nfsp_engine* e, bool pipelined, int par, bool snap_after)
     hipStream_t sa = e->s_br[a];
     NFSP_HIP(hipStreamWaitEvent(sa, serial_ar ? ar_done : fork_br, 0));
     KTimer kspan(e, KT_BR_STREAM0 + a, sa);     // this agent's BR stream, end to end
-    for (const Segment& sg : L.seg[a]) {
+    for (size_t gi = 0; gi < L.seg[a].size(); ++gi) {
+      const Segment& sg = L.seg[a][gi];
       {
         KTimer kt2(e, KT_TARGETS, sa);
         k_br_targets<<<(unsigned)(sg.v - sg.u), 256, 0, sa>>>(nullptr, br_target_job(e, L, a, sg),
@@ -740,6 +745,8 @@ static int update_impl(nfsp_engine* e, bool pipelined, int par, bool snap_after)
       C.B = cfg.batch;
       C.E = cfg.epochs;
       C.job[0] = br_chain_job(e, a, sg);
+      if (snap_after && gi + 1 == L.seg[a].size())            // the last segment writes the snapshot
+        C.job[0].snap_to = snap + (a * 3 + 1) * nn::NP;
       KTimer kc(e, KT_CHAIN_BR, sa);
       if ((rc = launch_br_chain(C, 1, cfg.quirks, e->log_loss, sa)) != NFSP_OK) return rc;
     }
@@ -748,8 +755,9 @@ static int update_impl(nfsp_engine* e, bool pipelined, int par, bool snap_after)
       NFSP_LAUNCHED("k_finalize");
     }
     if (snap_after) {
-      NFSP_HIP(hipMemcpyAsync(snap + (a * 3 + 1) * nn::NP, e->w + (a * 3 + 1) * nn::NP,
-                              sizeof(float) * nn::NP, hipMemcpyDeviceToDevice, sa));
+      if (L.seg[a].empty())             // no BR chain this call: copy the net as it is
+        NFSP_HIP(hipMemcpyAsync(snap + (a * 3 + 1) * nn::NP, e->w + (a * 3 + 1) * nn::NP,
+                                sizeof(float) * nn::NP, hipMemcpyDeviceToDevice, sa));
       NFSP_HIP(hipEventRecord(e->snap_ev[par][1 + a], sa));
     }
   }

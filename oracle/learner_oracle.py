@@ -110,11 +110,13 @@ def bits_to_x(bits):
     return ((bits[:, None] >> np.arange(30)) & 1).astype(np.float32)
 
 
-def ar_minibatches(cfg, state, a, quirks=7, slots=None):
+def ar_minibatches(cfg, state, a, quirks=7, slots=None, build_below=None):
     """The AR updates of agent a's learner call, in order: yields (u, bits [B], targets [B, 3],
     perms [E, B]) -- M_SL as of the trigger (k_ar_prep) -- or (u, None, None, None) for an
     update skipped because M_SL holds <= batch records.  The inputs of an AR update do not
-    depend on the weights, so any stretch of the chain can be replayed from given weights."""
+    depend on the weights, so any stretch of the chain can be replayed from given weights.
+    build_below: only updates u < build_below get their minibatch drawn; later active ones
+    yield (u, True, None, None) (a replayed prefix only needs their count)."""
     c, B, E = cfg["c"], cfg["batch"], cfg["epochs"]
     k0, k1 = cfg["seed"] & M32, (cfg["seed"] >> 32) & M32
     st = state[a]
@@ -139,6 +141,9 @@ def ar_minibatches(cfg, state, a, quirks=7, slots=None):
         count = min(sl0 + nb, cap)
         if count <= B:
             yield u, None, None, None
+            continue
+        if build_below is not None and u >= build_below:
+            yield u, True, None, None
             continue
         picks = sample_distinct(B, 0, count, TAG_SAMPLE | (a * 2), m, k0, k1)
         xb = np.empty(B, np.int64)
@@ -229,7 +234,7 @@ def learner_step(cfg, state, quirks=7, max_updates=None, trace=None):
         cap = cfg["sl_capacity"]
         slots = reservoir_slots(a, sl0, n_sl, cap, k0, k1, quirks)
         n_ar = 0
-        for u, xb, ya, perms in ar_minibatches(cfg, state, a, quirks, slots):
+        for u, xb, ya, perms in ar_minibatches(cfg, state, a, quirks, slots, build_below=lim(U)):
             if xb is None:
                 continue
             n_ar += 1
