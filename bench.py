@@ -578,6 +578,16 @@ def main():
     out["exploitability_exact"] = {
         "softmax_mixed": ex[0]["exploitability"], "argmax_as_executed": ex[1]["exploitability"],
         "hands_trained_per_gpu": int(s2["hands"]), "unit": "chips (BR_0 + BR_1)"}
+    band_path = os.path.join(REPO, "tests", "golden", "cpu_band_c3mem.json")
+    if cfg.get("game", "leduc") == "leduc" and cfg["rl_capacity"] == 200_000 and os.path.exists(band_path):
+        # the CPU reference's seed band at the same hands (main.train in C++, C3's memories,
+        # 8 seeds: tests/golden/cpu_band_c3mem.json; one seed of the engine here)
+        with open(band_path) as f:
+            cb = json.load(f)["band"]
+        h = min((int(k) for k in cb), key=lambda k: abs(k - int(s2["hands"])))
+        out["exploitability_exact"]["cpu_band_at_hands"] = {
+            "hands": h, "mean": cb[str(h)][0], "std": cb[str(h)][1],
+            "source": "tests/golden/cpu_band_c3mem.json (8 seeds)"}
     if world == 1 and args.config == "c3" and args.groups:
         # several learners on the one GPU (engine groups): new measured configs, not the headline
         eng.close()

@@ -289,6 +289,11 @@ int nfsp_engine_destroy(nfsp_engine* e);
  * 1 = BR best_response_model, 2 = target_br_model); read or write them in place. */
 int nfsp_engine_weights(nfsp_engine* e, int agent, int net, float** dev_w);
 int nfsp_rollout(nfsp_engine* e);
+/* Test hook: nfsp_rollout acting with the given nets (device [2 agents][3 nets][NP], the
+ * target slots unused) and epsilons instead of the engine's -- what a pipelined slice does
+ * with its snapshot (cfg.slice_lag 2); lets a test drive a lag-1 engine through the same
+ * schedule and compare. */
+int nfsp_rollout_with(nfsp_engine* e, const float* dev_w, const double* eps /*[2]*/);
 int nfsp_engine_update(nfsp_engine* e);
 int nfsp_engine_step(nfsp_engine* e);          /* nfsp_rollout + nfsp_engine_update */
 /* After a non-OK return from nfsp_rollout / nfsp_engine_update / nfsp_engine_step the

@@ -747,6 +747,13 @@ int group_rollout_launch(nfsp_engine* const* eng, int R, const void* d_tab) {
 }  // namespace eng
 }  // namespace nfsp
 
+extern "C" int nfsp_rollout_with(nfsp_engine* e, const float* dev_w, const double* eps) {
+  NFSP_REQUIRE(e && dev_w && eps, "null argument");
+  NFSP_REQUIRE(e->s_ar, "a replica of an engine group is stepped by nfsp_group_step");
+  const double ev[2] = {eps[0], eps[1]};
+  return nfsp::eng::rollout_launch_with(e, dev_w, ev);
+}
+
 extern "C" int nfsp_rollout(nfsp_engine* e) {
   NFSP_REQUIRE(e, "null argument");
   NFSP_REQUIRE(e->s_ar, "a replica of an engine group is stepped by nfsp_group_step");

@@ -101,6 +101,15 @@ class SelfPlayEngine:
     def rollout(self):
         native.check(self.L.nfsp_rollout(self.h), "nfsp_rollout")
 
+    def rollout_with(self, w_flat: np.ndarray, eps):
+        """Test hook (nfsp_rollout_with): the next slice's rollout acting with the given nets
+        ([2][3][NP] flat, as weights_tensor packs them) and epsilons."""
+        w = torch.as_tensor(np.asarray(w_flat, np.float32).reshape(-1), device=self.dev)
+        assert w.numel() == 6 * NP
+        e = (C.c_double * 2)(float(eps[0]), float(eps[1]))
+        native.check(self.L.nfsp_rollout_with(self.h, C.c_void_p(w.data_ptr()), e), "nfsp_rollout_with")
+        torch.cuda.synchronize(self.dev)       # w is a temporary
+
     def update(self):
         native.check(self.L.nfsp_engine_update(self.h), "nfsp_engine_update")
 

@@ -96,6 +96,7 @@ SIGNATURES = {
     "nfsp_engine_destroy": (I32, [P]),
     "nfsp_engine_weights": (I32, [P, I32, I32, PP]),
     "nfsp_rollout": (I32, [P]),
+    "nfsp_rollout_with": (I32, [P, P, P]),
     "nfsp_engine_update": (I32, [P]),
     "nfsp_engine_step": (I32, [P]),
     "nfsp_engine_get_stats": (I32, [P, C.POINTER(EngineStats)]),

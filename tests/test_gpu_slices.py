@@ -245,3 +245,35 @@ def test_c4_emulated_learns_within_the_cpu_seed_band(pkg):
     for (h, near, cm, cs, gm, gs) in report:
         assert abs(gm - cm) <= 2 * cs, report
         assert gm <= cm + cs, report
+
+
+def test_pipelined_step_equals_its_declared_schedule(pkg):
+    """cfg.slice_lag 2 is exactly its declared semantics: a lag-1 engine driven slice by slice
+    -- slice j's rollout acting with the nets and epsilon left by slice j - 2's learner (the
+    step's start for j < 2, nfsp_rollout_with), then its learner -- ends every step with the
+    same nets, counters and memories, bit for bit, as the pipelined engine."""
+    K = 4
+    kw = dict(n_lanes=32_768, slices=K, rl_capacity=20_000, sl_capacity=30_000, seed=4711, init_seed=9,
+              target_every=13)
+    a = pkg.engine.SelfPlayEngine(slice_lag=2, **kw)
+    b = pkg.engine.SelfPlayEngine(slice_lag=1, **kw)
+    for step in range(3):
+        a.step()
+        snap = [_weights_flat(b)] * 2
+        eps = [tuple(float(v) for v in b.stats()["epsilon"])] * 2
+        for j in range(K):
+            b.rollout_with(snap[j & 1], eps[j & 1])
+            b.update()
+            if j + 2 < K:
+                snap[j & 1] = _weights_flat(b)
+                eps[j & 1] = tuple(float(v) for v in b.stats()["epsilon"])
+        sa, sb = a.stats(), b.stats()
+        assert sa == sb, (step, {k: (sa[k], sb[k]) for k in sa if sa[k] != sb[k]})
+        assert np.array_equal(_weights_flat(a), _weights_flat(b)), step
+    assert min(sa["br_updates"]) > 50 and sa["target_syncs"][0] > 3
+    for p in (0, 1):
+        ma, mb = _logical_rl(a, p), _logical_rl(b, p)
+        for k in ma:
+            assert np.array_equal(ma[k], mb[k]), (p, k)
+        n = int(sa["sl_size"][p])
+        assert np.array_equal(a.memories(p)["sl_a"][:n].cpu().numpy(), b.memories(p)["sl_a"][:n].cpu().numpy())
