@@ -63,9 +63,9 @@ CONFIGS = {
     "c3_1slice": dict(n_lanes=1_048_576, rl_capacity=200_000, sl_capacity=2_000_000,
                       label="C3 with all 1,048,576 lanes in one rollout per step (round 2's form: policy "
                             "lag of 1M hands), M_RL 200k + M_SL 2M, reference cadence"),
-    "c2": dict(n_lanes=65_536, rl_capacity=40_000, sl_capacity=40_000,
-               label="C2: 65,536 Leduc lanes/GPU, M_RL/M_SL 40k, eta 0.1, 2x64 MLP heads, "
-                     "reference update cadence"),
+    "c2": dict(n_lanes=65_536, slices=16, slice_lag=2, rl_capacity=40_000, sl_capacity=40_000,
+               label="C2: 65,536 Leduc lanes/GPU (16 pipelined slices of 4,096), M_RL/M_SL 40k, "
+                     "eta 0.1, 2x64 MLP heads, reference update cadence"),
     "c3_4k": dict(n_lanes=4_096, rl_capacity=200_000, sl_capacity=2_000_000,
                   label="C3's memories and cadence at 4,096 lanes (policy lag 4k hands; DESIGN §9)"),
     "c3_64k": dict(n_lanes=65_536, rl_capacity=200_000, sl_capacity=2_000_000,
@@ -79,11 +79,13 @@ CONFIGS = {
                               f"each with device M_RL 200k + M_SL 2M, target sync 150, reference cadence; "
                               f"AR nets averaged over the replicas every step")
        for R in (2, 4, 8, 16, 32, 64, 128, 256)},
-    "c5": dict(n_lanes=1_048_576, rl_capacity=200_000, sl_capacity=2_000_000, game="kuhn",
-               label="C5: Kuhn swap-in, 1,048,576 lanes/GPU, C3's memories and cadence"),
+    "c5": dict(n_lanes=1_048_576, slices=16, slice_lag=2, rl_capacity=200_000, sl_capacity=2_000_000,
+               game="kuhn", label="C5: Kuhn swap-in, 1,048,576 lanes/GPU (16 pipelined slices), C3's "
+                                  "memories and cadence"),
     # C5's exploitability -> 0 check runs textbook NFSP with the MSE Q loss
-    "c5_tb": dict(n_lanes=1_048_576, rl_capacity=200_000, sl_capacity=2_000_000, game="kuhn", quirks=504,
-                  label="C5: Kuhn swap-in, 1,048,576 lanes/GPU, C3's memories and cadence, "
+    "c5_tb": dict(n_lanes=1_048_576, slices=16, slice_lag=2, rl_capacity=200_000, sl_capacity=2_000_000,
+                  game="kuhn", quirks=504,
+                  label="C5: Kuhn swap-in, 1,048,576 lanes/GPU (16 pipelined slices), C3's memories and cadence, "
                         "textbook NFSP with the MSE Q loss (quirks NFSP_TEXTBOOK_MSE)"),
 }
 

@@ -214,3 +214,19 @@ def test_gpu_kuhn_c5_exploitability_toward_zero(pkg):
         eng.step()
     e1 = eng.exploitability(0)["exploitability"]
     assert e0 > 1.0 and e1 < 0.15, (e0, e1)
+
+
+@pytest.mark.gpu
+def test_gpu_kuhn_c5_sliced_reaches_the_plateau_in_a_third_of_the_hands(pkg):
+    """bench.py's C5-textbook form: the same 1,048,576 lanes advanced in 16 pipelined slices
+    (cfg.slices 16, slice_lag 2: policy lag 128k hands instead of 1M).  Measured over 4 seeds
+    (profiles/r03_kuhn_tb_slices.json): 0.091 +- 0.009 chips after 12 steps (12.6M hands),
+    where the one-rollout form is at 0.280 +- 0.076 and needs ~40 steps to reach 0.11.  Bar:
+    below 0.13 after 12 steps (one seed; > 4 sigma above the measured mean)."""
+    eng = pkg.engine.SelfPlayEngine(n_lanes=1_048_576, rl_capacity=200_000, sl_capacity=2_000_000,
+                                    seed=1234, init_seed=0, game=pkg.native.GAME_KUHN,
+                                    quirks=pkg.native.TEXTBOOK_MSE, slices=16, slice_lag=2)
+    for _ in range(12):
+        eng.step()
+    e1 = eng.exploitability(0)["exploitability"]
+    assert e1 < 0.13, e1
