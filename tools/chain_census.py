@@ -37,12 +37,16 @@ def asm(src):
 
 
 def loop_body(lines, kernel):
+    """The step loop's instructions from its header to its back edge.  Blocks placed after the
+    back edge (the AR chain's rarely taken clipped-softmax block) are not counted: the census
+    is the common path."""
     start = next(i for i, l in enumerate(lines) if l.startswith(kernel))
+    stop = next(i for i in range(start, len(lines)) if lines[i].startswith(".Lfunc_end"))
     best = None
-    for h in [i for i in range(start, len(lines)) if "Loop Header" in lines[i]][:8]:
+    for h in [i for i in range(start, stop) if "Loop Header" in lines[i]]:
         lab = lines[h].split(":")[0]
-        end = next((i for i in range(h, min(len(lines), h + 4000))
-                    if re.search(r"s_cbranch_\w+\s+" + re.escape(lab) + r"\s*$", lines[i])), None)
+        end = next((i for i in range(h, stop)
+                    if re.search(r"s_(cbranch_\w+|branch)\s+" + re.escape(lab) + r"\s*$", lines[i])), None)
         if end is None:
             continue
         body = [l.strip() for l in lines[h + 1:end + 1]
