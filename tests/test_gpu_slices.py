@@ -8,7 +8,9 @@ update trigger agent/agent.py:153-154).
   global lane id and the lane's hand count): with the learner off, a sliced engine fills
   M_RL and M_SL exactly like an unsliced one, record for record;
 * at C3 size with the learner on, sampled lanes of the sliced rollouts replay bit-exact
-  through oracle/rollout_oracle.py (global lane ids, hand index = rollouts // slices);
+  through oracle/rollout_oracle.py (global lane ids, hand index = rollouts // slices); with
+  pipelined slices (slice_lag 2) against the snapshot they acted with, for Leduc and for
+  bench.py's C5-textbook form (Kuhn, NFSP_TEXTBOOK_MSE);
 * the C3 learning gate: exact exploitability after 8M / 16M / 25M / 33M hands at C3 (1M
   lanes, 16 slices, M_RL 200k, M_SL 2M) against the CPU seed band of the reference's
   main.train restated in C++ with the same memories and initial nets
@@ -66,7 +68,7 @@ def test_slicing_leaves_every_hand_unchanged(pkg):
         assert np.array_equal(xa["sl_a"][:n].cpu().numpy(), xb["sl_a"][:n].cpu().numpy())
 
 
-def _check_slice_lanes(eng, seed, lanes, rl_before, w=None, eps=None):
+def _check_slice_lanes(eng, seed, lanes, rl_before, w=None, eps=None, game="leduc"):
     """Sampled local lanes of the last rollout vs the oracle's replay of their global lanes
     (acting nets / epsilon: the engine's current ones unless given)."""
     lane0, g = eng.last_slice()
@@ -80,7 +82,8 @@ def _check_slice_lanes(eng, seed, lanes, rl_before, w=None, eps=None):
     eps = (float(st["epsilon"][0]), float(st["epsilon"][1])) if eps is None else eps
     mems = [eng.memories(p) for p in (0, 1)]
     for L in lanes:
-        ref = R._one_lane(lane0 + L, g, seed, w, eps, eng.cfg.eta, True)
+        q = int(eng.cfg.quirks)
+        ref = R._one_lane(lane0 + L, g, seed, w, eps, eng.cfg.eta, bool(q & 4), game, ext=q)
         for p in (0, 1):
             m = mems[p]
             n = len(ref["rl"][p])
@@ -147,6 +150,24 @@ def test_pipelined_slices_act_with_the_nets_two_slices_back(pkg, K):
     assert eng.last_slice() == ((K - 1) * eng.slice_lanes, 1)
     before = tuple(int(st["rl_total"][p] - st["last_rl"][p]) for p in (0, 1))
     _check_slice_lanes(eng, seed, _sample_lanes(eng.slice_lanes, 48, 20 + K), before, w, eps)
+
+
+def test_kuhn_textbook_pipelined_slices_replay_on_the_oracle(pkg):
+    """bench.py's C5-textbook form (Kuhn, NFSP_TEXTBOOK_MSE, 16 pipelined slices) at 262,144
+    lanes: the last slice of the second step replays bit-exact with the snapshot it acted with
+    (sampled AR actions, reservoir M_SL, constant epsilon included)."""
+    seed, K = 4242, 16
+    eng = pkg.engine.SelfPlayEngine(seed=seed, init_seed=2, slices=K, slice_lag=2, n_lanes=262_144,
+                                    rl_capacity=200_000, sl_capacity=2_000_000,
+                                    game=pkg.native.GAME_KUHN, quirks=pkg.native.TEXTBOOK_MSE)
+    eng.step()
+    eng.step()
+    st = eng.stats()
+    assert st["rollouts"] == 2 * K and min(st["br_updates"]) > 100
+    w, eps = eng.snapshot((K - 1) & 1)
+    assert eng.last_slice() == ((K - 1) * eng.slice_lanes, 1)
+    before = tuple(int(st["rl_total"][p] - st["last_rl"][p]) for p in (0, 1))
+    _check_slice_lanes(eng, seed, _sample_lanes(eng.slice_lanes, 48, 77), before, w, eps, game="kuhn")
 
 
 def test_pipelined_step_is_deterministic(pkg):
