@@ -1,7 +1,9 @@
 """C4's AR-gradient all-reduce on real engines (shards.AvgPolicyAllReduce over the device
 weight views): two shards co-resident on one GPU, gloo between them (the one-GPU box has
 no second device for RCCL).  After each engine step every shard holds W0 + mean_r(W_r - W0)
-for both agents' AR nets; the BR nets stay per shard."""
+for both agents' AR nets; the BR nets stay per shard.  Two sizes: 4,096 lanes, and C4's own
+shard (bench.py's C3 line per rank: 1,048,576 lanes in 16 pipelined slices, M_RL 200k,
+M_SL 2M)."""
 import multiprocessing as mp
 import os
 import socket
@@ -19,7 +21,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, q):
+SIZES = {"4k": dict(n_lanes=4096, rl_capacity=40_000, sl_capacity=40_000),
+         "c4": dict(n_lanes=1_048_576, slices=16, slice_lag=2, rl_capacity=200_000,
+                    sl_capacity=2_000_000)}
+
+
+def _worker(rank, world, port, q, size):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                           WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
@@ -30,8 +37,7 @@ def _worker(rank, world, port, q):
         import __graft_entry__
         pkg = __graft_entry__.load_package()
         _, r, _, dist = bench.init_dist(backend="gloo")
-        eng = pkg.engine.SelfPlayEngine(n_lanes=4096, rl_capacity=40_000, sl_capacity=40_000,
-                                        seed=1234 + r, init_seed=r)
+        eng = pkg.engine.SelfPlayEngine(seed=1234 + r, init_seed=r, **SIZES[size])
         AR, BR = pkg.engine.NET_AR, pkg.engine.NET_BR
         avg = pkg.shards.AvgPolicyAllReduce([eng.weights_tensor(a, AR) for a in (0, 1)], dist,
                                             sync=torch.cuda.synchronize)
@@ -55,11 +61,12 @@ def _worker(rank, world, port, q):
 
 
 @pytest.mark.gpu
-def test_two_shards_share_the_average_policy():
+@pytest.mark.parametrize("size", ["4k", "c4"])
+def test_two_shards_share_the_average_policy(size):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, size)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=240) for _ in procs)
