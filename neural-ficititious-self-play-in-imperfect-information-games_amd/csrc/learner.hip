@@ -136,14 +136,13 @@ __device__ inline uint4 bits8u(uint32_t x, int g) {
                     ((n1 >> 2) & 1u) * 0x3F80u + ((n1 >> 3) & 1u) * 0x3F800000u);
 }
 
-// The chain records of one (update, epoch): thread b holds fit position b's observation
-// mask x (for b < B), targets and the lr; minibatch b >> 5 gets fa / tg of its sample
-// b & 31, and ba from the bit transpose of its 32 masks by wave ballot.  Every valid
-// sample also carries the bias input (CHAIN_BIAS_BIT).  Whole block (a multiple of 64
-// threads) calls.
+// The chain records of one (update, epoch): the thread of fit position b holds its
+// observation mask x (for b < B), targets and the lr; minibatch b >> 5 gets fa / tg of its
+// sample b & 31, and ba from the bit transpose of its 32 masks by wave ballot.  Every valid
+// sample also carries the bias input (CHAIN_BIAS_BIT).  Called by whole waves whose lanes
+// hold positions b = 64 k + lane (k = 0, 1, ...: one record group of 64-thread waves).
 __device__ inline void emit_recs(StepRec* __restrict__ recs, uint32_t x, float t0, float t1, float t2,
-                                 float lr, int B) {
-  const int b = threadIdx.x;
+                                 float lr, int B, int b) {
   if (b < B) {
     x |= CHAIN_BIAS_BIT;
     StepRec& R = recs[b >> 5];
@@ -263,7 +262,7 @@ __global__ void __launch_bounds__(128) k_ar_prep(PrepArgs P0, const PrepArgs* __
     // targets / batch: the AR chain's cross-entropy gradient takes them pre-scaled (exact)
     const float sc = 1.0f / (float)CHAIN_MB;
     emit_recs(P.LB.ar_rec + (slot_u * P.E + e) * (P.B / CHAIN_MB), in ? px[b] : 0u, in ? pt[b][0] * sc : 0.f,
-              in ? pt[b][1] * sc : 0.f, in ? pt[b][2] * sc : 0.f, P.lr_ar, P.B);
+              in ? pt[b][1] * sc : 0.f, in ? pt[b][2] * sc : 0.f, P.lr_ar, P.B, b);
     __syncthreads();
   }
   if (last && b < P.B) P.M.dbg_rows[dbg * P.B + b] = cand[b];
@@ -323,6 +322,15 @@ __global__ void __launch_bounds__(256) k_br_targets(const TargetJob* __restrict_
   const int64_t u = J.u0 + blockIdx.x;
   BrRow rr{};
   if (b < B) rr = J.rows[u * B + b];
+  // the records of epoch e are emitted by threads 128 (e & 1) .. + 127 (below); their fit
+  // order is loaded now, beside the net
+  const int half = tid >> 7;
+  int pk[2] = {0, 0};
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int e = half + 2 * k;
+    if (e < E && b < B) pk[k] = J.perm[(u * E + e) * B + b];
+  }
   stage_net_lds(sw, J.tw, tid, blockDim.x);
   __syncthreads();
   if (b < B) {
@@ -369,15 +377,16 @@ __global__ void __launch_bounds__(256) k_br_targets(const TargetJob* __restrict_
   // lr of this update: lr0 / (1 + 0.003 sqrt(iteration)) with iteration = it0 + 2 u
   // (agent/agent.py:249, iteration += 2 per BR update), in the reference's double arithmetic
   const float lr = (float)(lr0 / (1.0 + 0.003 * sqrt((double)(J.it0 + 2 * u))));
-  for (int e = 0; e < E; ++e) {
+  // epochs in pairs: threads 0..127 emit epoch e, threads 128..255 epoch e + 1
+  for (int e = half, k = 0; e < E; e += 2, ++k) {
     uint32_t x = 0;
     float t0 = 0.f, t1 = 0.f, t2 = 0.f;
-    if (!s2half && b < B) {
-      const int k = J.perm[(u * E + e) * B + b];
-      x = sb[k];
-      t0 = q[k][0]; t1 = q[k][1]; t2 = q[k][2];
+    if (b < B) {
+      const int r = k < 2 ? pk[k] : J.perm[(u * E + e) * B + b];
+      x = sb[r];
+      t0 = q[r][0]; t1 = q[r][1]; t2 = q[r][2];
     }
-    emit_recs(J.rec + (u * E + e) * (B / CHAIN_MB), x, t0, t1, t2, lr, B);
+    emit_recs(J.rec + (u * E + e) * (B / CHAIN_MB), x, t0, t1, t2, lr, B, b);
   }
 }
 
