@@ -21,7 +21,8 @@ struct ChainJob {
   float* w;                       // weights of (agent, net)
   float* sync_to;                 // BR: target net to copy into at the end (or null)
   float* snap_to;                 // a pipelined slice's snapshot of the net (or null)
-  const StepRec* rec;             // this agent's step records [umax][E][B / 32] (prep kernels)
+  const void* rec;                // this agent's step records [umax][E][B / 32] (prep kernels):
+                                  // StepRec (BR), ArStepRec (AR)
   const uint8_t* active;          // AR: per-update flag, 0..0 1..1 in u (null for BR)
   float* loss_out;                // optional: [umax][E] Keras epoch losses (the values the
                                   // reference's TensorBoard callbacks log, agent/agent.py:84-88)
@@ -99,10 +100,12 @@ __device__ inline float sum_x16(float x) {
 //     backward and dW1) and Z1^T hidden-major (D row = hidden: layer 2 is then 4 lane-local
 //     FMAs per output plus two permlane swaps instead of a 16-lane reduction);
 //   * dW1 = X^T dZ1 with K = samples (K slot 8g + j <-> sample 16 (j >> 2) + 4g + (j & 3));
-//   * every bit operand comes ready-made from the step record (StepRec: the prep kernels
-//     expand the masks and their bit transpose).  Records pass through a 4-slot LDS ring:
-//     each wave loads a quarter of record t + 2 during step t, and step t + 1's barrier
-//     publishes it;
+//   * every bit operand comes ready-made from the step record (the prep kernels expand the
+//     masks to bf16 0/1 fragments).  Records pass through a 4-slot LDS ring: each wave loads
+//     a quarter of record t + 2 during step t, and step t + 1's barrier publishes it.  The BR
+//     record (StepRec) also carries the bit transpose (the dW1 operand X^T); the AR chain
+//     reads X^T from the fa image itself (ds_read_b64_tr_b16), so its record (ArStepRec) is
+//     fa + targets;
 //   * one barrier per step (the 4 waves' layer-2 partials); all other exchange is
 //     wave-private (LDS dm / w2t) or cross-lane (DPP, permlane).
 // ---------------------------------------------------------------------------
@@ -124,12 +127,17 @@ struct Chain3Smem {
   float4 w2t[4][64];         // wave-private: W2[h][0..2] of the slice (rows 0..15: the layer-2
                              // weights live here, each component written by the lanes owning it)
   float b2s[4][4];           // wave-private: b2
-  StepRec ring[4];           // step records t .. t + 2 (slot t & 3), a quarter per wave
+  StepRec ring[4];           // step records t .. t + 2 (slot t & 3), a quarter per wave (AR:
+                             // an ArStepRec at the start of each slot)
   uint4 rec_sink[64];
 };
-constexpr int REC_CHUNKS = (int)(sizeof(StepRec) / 16);    // 288 x 16 B
-constexpr int REC_QUARTER = REC_CHUNKS / 4;                 // 72 per wave
-static_assert(REC_CHUNKS % 4 == 0 && REC_QUARTER > 64 && REC_QUARTER <= 128, "record chunking");
+// record geometry of a chain: 16-byte chunks per record (BR 160, AR 152), a quarter per wave
+template <int RELU> constexpr int rec_chunks() {
+  return (int)((RELU ? sizeof(StepRec) : sizeof(ArStepRec)) / 16);
+}
+static_assert(rec_chunks<1>() % 4 == 0 && rec_chunks<1>() / 4 > 64 && rec_chunks<1>() / 4 <= 128,
+              "record chunking");
+static_assert(rec_chunks<0>() % 4 == 0 && rec_chunks<0>() / 4 <= 64, "record chunking");
 // Reserve (nearly) all of a CU's LDS for a chain workgroup: a chain then has its CU to
 // itself -- no prep / target kernel's waves share its SIMDs.
 constexpr int CHAIN_LDS = 150 * 1024;
@@ -221,6 +229,16 @@ __device__ inline void split3(const float (&v)[8], bf16x8& hi, bf16x8& mid, bf16
   lo = __builtin_bit_cast(bf16x8, make_uint4(o0, o1, o2, o3));
 }
 
+// 8 bf16 of a transposed operand: two ds_read_b64_tr_b16 (rows lo .. lo + 3, hi .. hi + 3 of
+// a 16-bit image in LDS; see T10 in cdna_hip_programming.md).  The whole wave must be active.
+typedef short short4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) short4v lds_short4v;
+__device__ inline bf16x8 tr_pair(const char* lo, const char* hi) {
+  const short4v a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4v*)lo);
+  const short4v b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_short4v*)hi);
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
 __device__ inline floatx4 mfma3(bf16x8 a, bf16x8 bhi, bf16x8 bmid, bf16x8 blo) {
   floatx4 z = {};
   z = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, blo, z, 0, 0, 0);
@@ -278,20 +296,30 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
   const int T1 = (int)(u1 * spu);
   int t = (int)(u0 * spu);
   const uint4* recb = reinterpret_cast<const uint4*>(J.rec);
-  // this wave's quarter of record p (clamped), into two registers / back into ring slot p & 3;
-  // the lanes past the quarter load a duplicate chunk and store it to the sink
-  const bool in_q = l < REC_QUARTER - 64;
-  const int lb = in_q ? 64 + l : REC_QUARTER - 1;
+  // this wave's quarter of record p (clamped), into registers / back into ring slot p & 3:
+  // BR (72 chunks) two per lane, AR (<= 64) one; the lanes past the quarter load a duplicate
+  // chunk and store it to the sink
+  constexpr int REC_CHUNKS = rec_chunks<RELU>(), REC_QUARTER = REC_CHUNKS / 4;
+  constexpr bool TWO = REC_QUARTER > 64;
+  const bool in_q = TWO ? l < REC_QUARTER - 64 : l < REC_QUARTER;
+  const int lb = in_q ? (TWO ? 64 : 0) + l : REC_QUARTER - 1;
   auto issue = [&](int p, uint4& va, uint4& vb) {
     const uint4* src = recb + (size_t)(p < T1 ? p : T1 - 1) * REC_CHUNKS + REC_QUARTER * w;
-    va = src[l];
+    if (TWO) va = src[l];
     vb = src[lb];
   };
   auto stash = [&](int p, const uint4& va, const uint4& vb) {
     uint4* dst = reinterpret_cast<uint4*>(&sm.ring[p & 3]) + REC_QUARTER * w;
-    dst[l] = va;
-    *(in_q ? dst + 64 + l : &sm.rec_sink[l]) = vb;
+    if (TWO) dst[l] = va;
+    *(in_q ? dst + (TWO ? 64 : 0) + l : &sm.rec_sink[l]) = vb;
   };
+  // AR: X^T (the dW1 operand, K = samples) by transposed reads of the fa image: in each
+  // 16-lane group g, lane c = 4q + p supplies row q = sample 4g + q, columns 4p .. 4p + 3 =
+  // inputs 4p .. 4p + 3, i.e. the first 8 bytes of sample 4g + q's chunk of row p; lane c
+  // receives input c of samples 4g .. 4g + 3.  +256 B: samples 16 + 4g ..; +8 B: inputs
+  // 16 + 4p .. (ba1: input 16 + c).
+  const int tr_off = 512 * (c & 3) + 16 * fa_slot(c & 3, 4 * g + (c >> 2));
+  const int fsw = RELU ? 0 : 12 * (g & 1);      // fa_slot(g, .) of the AR image
   auto publish = [&]() {   // this wave's W2 rows for its own Z1^T layer 2
     sm.w2t[w][l] = make_float4(W2_0, W2_1, W2_2, 0.f);
   };
@@ -318,10 +346,15 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
     uint4 va, vb;
     issue(t + 2, va, vb);
     const StepRec& R = sm.ring[t & 3];
-    const bf16x8 fa0 = __builtin_bit_cast(bf16x8, R.fa[g][c]);
-    const bf16x8 fa1 = __builtin_bit_cast(bf16x8, R.fa[g][16 + c]);
-    const bf16x8 ba0 = __builtin_bit_cast(bf16x8, R.ba[g][c]);
-    const bf16x8 ba1 = __builtin_bit_cast(bf16x8, R.ba[g][16 + c]);
+    const ArStepRec& RA = reinterpret_cast<const ArStepRec&>(R);
+    const bf16x8 fa0 = __builtin_bit_cast(bf16x8, R.fa[g][c ^ fsw]);
+    const bf16x8 fa1 = __builtin_bit_cast(bf16x8, R.fa[g][(16 + c) ^ fsw]);
+    bf16x8 ba0, ba1;
+    const char* const rtr = reinterpret_cast<const char*>(&RA.fa[0][0]) + tr_off;
+    if (RELU) {
+      ba0 = __builtin_bit_cast(bf16x8, R.ba[g][c]);
+      ba1 = __builtin_bit_cast(bf16x8, R.ba[g][16 + c]);
+    }
     // ---- layer 1, both orientations
     bf16x8 whi, wmid, wlo;
     split3(wr, whi, wmid, wlo, SK);
@@ -373,7 +406,7 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
     __builtin_amdgcn_sched_barrier(0);
     const floatx4 zs0 = mfma3(fa0, whi, wmid, wlo);      // Z1: sample 4g+r, hidden 16w+c
     const floatx4 zs1 = mfma3(fa1, whi, wmid, wlo);      //     sample 16+4g+r
-    const float4 tg = R.tg[sl];                          // read before the barrier pins it early
+    const float4 tg = RELU ? R.tg[sl] : RA.tg[sl];      // read before the barrier pins it early
     __builtin_amdgcn_sched_barrier(0);                   // ... and the Z1 MFMAs issue before it
     CHAIN_STAMP(1);
     __syncthreads();
@@ -490,6 +523,10 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
     for (int k = 0; k < 3; ++k) {
       dA[k] = *reinterpret_cast<const float4*>(&sm.dm[w][k][4 * g]);
       dB[k] = *reinterpret_cast<const float4*>(&sm.dm[w][k][16 + 4 * g]);
+    }
+    if (!RELU) {          // AR: X^T from the fa image, issued after the dm reads (measured
+      ba0 = tr_pair(rtr, rtr + 256);         // faster than beside the fa reads)
+      ba1 = tr_pair(rtr + 8, rtr + 264);
     }
     float dz[8];
     float g2_0 = 0.f, g2_1 = 0.f, g2_2 = 0.f;

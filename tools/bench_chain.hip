@@ -71,30 +71,41 @@ int main(int argc, char** argv) {
   for (auto& v : w) v = ud(rng);
   for (int i = nn::OW2; i < nn::NP; ++i) w[i] *= wscale;
   // step records, as k_br_targets / k_ar_prep emit them
-  std::vector<StepRec> rec((size_t)U * E * NMB);
-  for (size_t st = 0; st < rec.size(); ++st) {
+  // BR: StepRec (targets and lr per sample); AR: ArStepRec (targets by output, / batch)
+  const size_t nrec = (size_t)U * E * NMB;
+  const size_t rsz = relu ? sizeof(StepRec) : sizeof(ArStepRec);
+  std::vector<StepRec> br_rec(relu ? nrec : 0);
+  std::vector<ArStepRec> ar_rec(relu ? 0 : nrec);
+  for (size_t st = 0; st < nrec; ++st) {
     const int u = (int)(st / (E * NMB));
     const float lr = relu ? (float)(0.05 / (1.0 + 0.003 * sqrt((double)(2 * u)))) : 0.1f;
     uint32_t xt[32] = {0};
     for (int k = 0; k < 32; ++k) {
       const auto& r = fit[st * 32 + k];
       const uint32_t xb = r.x | CHAIN_BIAS_BIT;      // emit_recs: the bias input
-      for (int g = 0; g < 4; ++g) rec[st].fa[g][k] = bits8_host(xb, g);
-      const float ts = relu ? 1.f : 1.f / 32.f;        // AR records: targets / batch (k_ar_prep)
-      rec[st].tg[k] = make_float4(r.t0 * ts, r.t1 * ts, r.t2 * ts, lr);
-      for (int i = 0; i <= CHAIN_BIAS_IN; ++i) if ((xb >> i) & 1u) xt[i] |= 1u << k;
+      if (relu) {
+        for (int g = 0; g < 4; ++g) br_rec[st].fa[g][k] = bits8_host(xb, g);
+        br_rec[st].tg[k] = make_float4(r.t0, r.t1, r.t2, lr);
+        for (int i = 0; i <= CHAIN_BIAS_IN; ++i) if ((xb >> i) & 1u) xt[i] |= 1u << k;
+      } else {                                      // emit_ar_recs: targets / batch
+        for (int g = 0; g < 4; ++g) ar_rec[st].fa[g][fa_slot(g, k)] = bits8_host(xb, g);
+        ar_rec[st].tg[k] = make_float4(r.t0 / 32.f, r.t1 / 32.f, r.t2 / 32.f, lr);
+      }
     }
-    for (int i = 0; i < 32; ++i)
-      for (int g = 0; g < 4; ++g) rec[st].ba[g][i] = bits8_host(xt[i], g);
+    if (relu)
+      for (int i = 0; i < 32; ++i)
+        for (int g = 0; g < 4; ++g) br_rec[st].ba[g][i] = bits8_host(xt[i], g);
   }
-  chainref::FitRow* dfit; StepRec* drec; float* dw; unsigned long long* dst;
+  const void* rec_host = relu ? (const void*)br_rec.data() : (const void*)ar_rec.data();
+  const size_t rec_bytes = nrec * rsz;
+  chainref::FitRow* dfit; char* drec; float* dw; unsigned long long* dst;
   CK(hipMalloc(&dfit, fit.size() * sizeof(chainref::FitRow)));
-  CK(hipMalloc(&drec, rec.size() * sizeof(StepRec)));
+  CK(hipMalloc(&drec, rec_bytes));
   CK(hipMalloc(&dw, w.size() * 4));
   CK(hipMalloc(&dst, 80 * 8));
   CK(hipMemset(dst, 0, 80 * 8));
   CK(hipMemcpy(dfit, fit.data(), fit.size() * sizeof(chainref::FitRow), hipMemcpyHostToDevice));
-  CK(hipMemcpy(drec, rec.data(), rec.size() * sizeof(StepRec), hipMemcpyHostToDevice));
+  CK(hipMemcpy(drec, rec_host, rec_bytes, hipMemcpyHostToDevice));
   CK(hipMemcpy(dw, w.data(), w.size() * 4, hipMemcpyHostToDevice));
   float* dw2;
   CK(hipMalloc(&dw2, w.size() * 4));
@@ -112,14 +123,14 @@ int main(int argc, char** argv) {
   ChainJob* djobs = nullptr;
   if (nblk > 2) {
     std::vector<ChainJob> jobs(nblk, C.job[0]);
-    float* wall; StepRec* rall = drec;
+    float* wall; char* rall = drec;
     CK(hipMalloc(&wall, (size_t)nblk * w.size() * 4));
-    if (distinct) CK(hipMalloc(&rall, (size_t)nblk * rec.size() * sizeof(StepRec)));
+    if (distinct) CK(hipMalloc(&rall, (size_t)nblk * rec_bytes));
     for (int k = 0; k < nblk; ++k) {
       CK(hipMemcpy(wall + (size_t)k * w.size(), w.data(), w.size() * 4, hipMemcpyHostToDevice));
-      if (distinct) CK(hipMemcpy(rall + (size_t)k * rec.size(), rec.data(), rec.size() * sizeof(StepRec), hipMemcpyHostToDevice));
+      if (distinct) CK(hipMemcpy(rall + (size_t)k * rec_bytes, rec_host, rec_bytes, hipMemcpyHostToDevice));
       jobs[k].w = wall + (size_t)k * w.size();
-      jobs[k].rec = rall + (distinct ? (size_t)k * rec.size() : 0);
+      jobs[k].rec = rall + (distinct ? (size_t)k * rec_bytes : 0);
     }
     CK(hipMalloc(&djobs, sizeof(ChainJob) * nblk));
     CK(hipMemcpy(djobs, jobs.data(), sizeof(ChainJob) * nblk, hipMemcpyHostToDevice));
