@@ -217,7 +217,13 @@ __device__ __forceinline__ void rollout_body(const RolloutArgs& A, int bx) {
                                        (unsigned long long)(long long)s_rew[tid]);
 }
 
-__global__ void __launch_bounds__(256) k_rollout(RolloutArgs A) { rollout_body(A, blockIdx.x); }
+// One engine's rollout runs 512-lane workgroups (8 waves): a 65,536-lane slice then takes
+// 128 CUs instead of all 256.  Each rollout workgroup holds 38 KB of LDS (the four nets), so a
+// CU running one cannot take a chain workgroup (150 KB, chain3.h CHAIN_LDS); with every CU
+// holding one, a BR chain launched during the rollout waited for it to drain (~86 us, once
+// per slice on agent 0's BR stream: 1.3 ms per C3 step).
+constexpr int ROLLOUT_WG = 512;
+__global__ void __launch_bounds__(ROLLOUT_WG) k_rollout(RolloutArgs A) { rollout_body(A, blockIdx.x); }
 
 // engine groups: blockIdx.y = replica (the rollout index is the same for every replica)
 __global__ void __launch_bounds__(256) k_rollout_g(const GroupRollout* __restrict__ tab, uint32_t g_lo,
@@ -675,7 +681,7 @@ int rollout_launch_with(nfsp_engine* e, const float* w, const double eps[2]) {
   A.eps_v[1] = eps[1];
   {
     KTimer kt(e, KT_ROLLOUT);
-    k_rollout<<<e->nblk, 256, 0, s>>>(A);
+    k_rollout<<<(e->N + ROLLOUT_WG - 1) / ROLLOUT_WG, ROLLOUT_WG, 0, s>>>(A);
   }
   NFSP_LAUNCHED("k_rollout");
   {
