@@ -21,8 +21,7 @@ struct ChainJob {
   float* w;                       // weights of (agent, net)
   float* sync_to;                 // BR: target net to copy into at the end (or null)
   float* snap_to;                 // a pipelined slice's snapshot of the net (or null)
-  const void* rec;                // this agent's step records [umax][E][B / 32] (prep kernels):
-                                  // StepRec (BR), ArStepRec (AR)
+  const StepRec* rec;             // this agent's step records [umax][E][B / 32] (prep kernels)
   const uint8_t* active;          // AR: per-update flag, 0..0 1..1 in u (null for BR)
   float* loss_out;                // optional: [umax][E] Keras epoch losses (the values the
                                   // reference's TensorBoard callbacks log, agent/agent.py:84-88)
@@ -100,12 +99,11 @@ __device__ inline float sum_x16(float x) {
 //     backward and dW1) and Z1^T hidden-major (D row = hidden: layer 2 is then 4 lane-local
 //     FMAs per output plus two permlane swaps instead of a 16-lane reduction);
 //   * dW1 = X^T dZ1 with K = samples (K slot 8g + j <-> sample 16 (j >> 2) + 4g + (j & 3));
-//   * every bit operand comes ready-made from the step record (the prep kernels expand the
-//     masks to bf16 0/1 fragments).  Records pass through a 4-slot LDS ring: each wave loads
-//     a quarter of record t + 2 during step t, and step t + 1's barrier publishes it.  The BR
-//     record (StepRec) also carries the bit transpose (the dW1 operand X^T); the AR chain
-//     reads X^T from the fa image itself (ds_read_b64_tr_b16), so its record (ArStepRec) is
-//     fa + targets;
+//   * every bit operand comes ready-made from the step record (StepRec: the prep kernels
+//     expand the masks to bf16 0/1 fragments).  Records pass through a 4-slot LDS ring:
+//     each wave loads a quarter of record t + 2 during step t, and step t + 1's barrier
+//     publishes it.  The dW1 operand X^T is the same fa image read transposed
+//     (ds_read_b64_tr_b16), so a record is the fa image and the targets, 2,560 B;
 //   * one barrier per step (the 4 waves' layer-2 partials); all other exchange is
 //     wave-private (LDS dm / w2t) or cross-lane (DPP, permlane).
 // ---------------------------------------------------------------------------
@@ -127,17 +125,12 @@ struct Chain3Smem {
   float4 w2t[4][64];         // wave-private: W2[h][0..2] of the slice (rows 0..15: the layer-2
                              // weights live here, each component written by the lanes owning it)
   float b2s[4][4];           // wave-private: b2
-  StepRec ring[4];           // step records t .. t + 2 (slot t & 3), a quarter per wave (AR:
-                             // an ArStepRec at the start of each slot)
+  StepRec ring[4];           // step records t .. t + 2 (slot t & 3), a quarter per wave
   uint4 rec_sink[64];
 };
-// record geometry of a chain: 16-byte chunks per record (BR 160, AR 152), a quarter per wave
-template <int RELU> constexpr int rec_chunks() {
-  return (int)((RELU ? sizeof(StepRec) : sizeof(ArStepRec)) / 16);
-}
-static_assert(rec_chunks<1>() % 4 == 0 && rec_chunks<1>() / 4 > 64 && rec_chunks<1>() / 4 <= 128,
-              "record chunking");
-static_assert(rec_chunks<0>() % 4 == 0 && rec_chunks<0>() / 4 <= 64, "record chunking");
+constexpr int REC_CHUNKS = (int)(sizeof(StepRec) / 16);    // 160 x 16 B
+constexpr int REC_QUARTER = REC_CHUNKS / 4;                 // 40 per wave: one chunk per lane
+static_assert(REC_CHUNKS % 4 == 0 && REC_QUARTER <= 64, "record chunking");
 // Reserve (nearly) all of a CU's LDS for a chain workgroup: a chain then has its CU to
 // itself -- no prep / target kernel's waves share its SIMDs.
 constexpr int CHAIN_LDS = 150 * 1024;
@@ -296,30 +289,25 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
   const int T1 = (int)(u1 * spu);
   int t = (int)(u0 * spu);
   const uint4* recb = reinterpret_cast<const uint4*>(J.rec);
-  // this wave's quarter of record p (clamped), into registers / back into ring slot p & 3:
-  // BR (72 chunks) two per lane, AR (<= 64) one; the lanes past the quarter load a duplicate
-  // chunk and store it to the sink
-  constexpr int REC_CHUNKS = rec_chunks<RELU>(), REC_QUARTER = REC_CHUNKS / 4;
-  constexpr bool TWO = REC_QUARTER > 64;
-  const bool in_q = TWO ? l < REC_QUARTER - 64 : l < REC_QUARTER;
-  const int lb = in_q ? (TWO ? 64 : 0) + l : REC_QUARTER - 1;
-  auto issue = [&](int p, uint4& va, uint4& vb) {
+  // this wave's quarter of record p (clamped), into a register / back into ring slot p & 3;
+  // the lanes past the quarter load a duplicate chunk and store it to the sink
+  const bool in_q = l < REC_QUARTER;
+  const int la = in_q ? l : REC_QUARTER - 1;
+  auto issue = [&](int p, uint4& va) {
     const uint4* src = recb + (size_t)(p < T1 ? p : T1 - 1) * REC_CHUNKS + REC_QUARTER * w;
-    if (TWO) va = src[l];
-    vb = src[lb];
+    va = src[la];
   };
-  auto stash = [&](int p, const uint4& va, const uint4& vb) {
+  auto stash = [&](int p, const uint4& va) {
     uint4* dst = reinterpret_cast<uint4*>(&sm.ring[p & 3]) + REC_QUARTER * w;
-    if (TWO) dst[l] = va;
-    *(in_q ? dst + (TWO ? 64 : 0) + l : &sm.rec_sink[l]) = vb;
+    *(in_q ? dst + l : &sm.rec_sink[l]) = va;
   };
-  // AR: X^T (the dW1 operand, K = samples) by transposed reads of the fa image: in each
-  // 16-lane group g, lane c = 4q + p supplies row q = sample 4g + q, columns 4p .. 4p + 3 =
-  // inputs 4p .. 4p + 3, i.e. the first 8 bytes of sample 4g + q's chunk of row p; lane c
-  // receives input c of samples 4g .. 4g + 3.  +256 B: samples 16 + 4g ..; +8 B: inputs
-  // 16 + 4p .. (ba1: input 16 + c).
+  // X^T (the dW1 operand, K = samples) by transposed reads of the fa image: in each 16-lane
+  // group g, lane c = 4q + p supplies row q = sample 4g + q, columns 4p .. 4p + 3 = inputs
+  // 4p .. 4p + 3, i.e. the first 8 bytes of sample 4g + q's chunk of row p; lane c receives
+  // input c of samples 4g .. 4g + 3.  +256 B: samples 16 + 4g ..; +8 B: inputs 16 + 4p ..
+  // (ba1: input 16 + c).
   const int tr_off = 512 * (c & 3) + 16 * fa_slot(c & 3, 4 * g + (c >> 2));
-  const int fsw = RELU ? 0 : 12 * (g & 1);      // fa_slot(g, .) of the AR image
+  const int fsw = 12 * (g & 1);                // fa_slot(g, .) of this lane row
   auto publish = [&]() {   // this wave's W2 rows for its own Z1^T layer 2
     sm.w2t[w][l] = make_float4(W2_0, W2_1, W2_2, 0.f);
   };
@@ -343,18 +331,16 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
   // waves share one copy of each record.
   float loss_acc = 0.f;                        // wave 0 lane 0: running epoch loss
   auto step = [&]() {
-    uint4 va, vb;
-    issue(t + 2, va, vb);
+    uint4 va;
+    issue(t + 2, va);
     const StepRec& R = sm.ring[t & 3];
-    const ArStepRec& RA = reinterpret_cast<const ArStepRec&>(R);
     const bf16x8 fa0 = __builtin_bit_cast(bf16x8, R.fa[g][c ^ fsw]);
     const bf16x8 fa1 = __builtin_bit_cast(bf16x8, R.fa[g][(16 + c) ^ fsw]);
+    // X^T, read where each chain measured fastest (tools/chain_ab.sh; results identical):
+    // BR right after the barrier, AR after the dm reads.  Beside the fa reads both were
+    // slower (BR 0.831 -> 0.90 us, bimodal), as was carrying them from the previous step.
     bf16x8 ba0, ba1;
-    const char* const rtr = reinterpret_cast<const char*>(&RA.fa[0][0]) + tr_off;
-    if (RELU) {
-      ba0 = __builtin_bit_cast(bf16x8, R.ba[g][c]);
-      ba1 = __builtin_bit_cast(bf16x8, R.ba[g][16 + c]);
-    }
+    const char* const rtr = reinterpret_cast<const char*>(&R.fa[0][0]) + tr_off;
     // ---- layer 1, both orientations
     bf16x8 whi, wmid, wlo;
     split3(wr, whi, wmid, wlo, SK);
@@ -406,11 +392,15 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
     __builtin_amdgcn_sched_barrier(0);
     const floatx4 zs0 = mfma3(fa0, whi, wmid, wlo);      // Z1: sample 4g+r, hidden 16w+c
     const floatx4 zs1 = mfma3(fa1, whi, wmid, wlo);      //     sample 16+4g+r
-    const float4 tg = RELU ? R.tg[sl] : RA.tg[sl];      // read before the barrier pins it early
+    const float4 tg = R.tg[sl];                          // read before the barrier pins it early
     __builtin_amdgcn_sched_barrier(0);                   // ... and the Z1 MFMAs issue before it
     CHAIN_STAMP(1);
     __syncthreads();
     CHAIN_STAMP(2);
+    if (RELU) {
+      ba0 = tr_pair(rtr, rtr + 256);
+      ba1 = tr_pair(rtr + 8, rtr + 264);
+    }
     // ---- output + loss of sample sl (every wave redundantly, identical results)
     float d0, d1, d2, lr_step;
     float o_keep[3], tt_keep[3], p_keep[3];     // for the optional loss log
@@ -524,8 +514,8 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
       dA[k] = *reinterpret_cast<const float4*>(&sm.dm[w][k][4 * g]);
       dB[k] = *reinterpret_cast<const float4*>(&sm.dm[w][k][16 + 4 * g]);
     }
-    if (!RELU) {          // AR: X^T from the fa image, issued after the dm reads (measured
-      ba0 = tr_pair(rtr, rtr + 256);         // faster than beside the fa reads)
+    if (!RELU) {
+      ba0 = tr_pair(rtr, rtr + 256);
       ba1 = tr_pair(rtr + 8, rtr + 264);
     }
     float dz[8];
@@ -578,16 +568,16 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
       wr[r] = wr[r] - lr * gA[r];
       wr[4 + r] = wr[4 + r] - lr * gB[r];
     }
-    stash(t + 2, va, vb);
+    stash(t + 2, va);
     CHAIN_STAMP(5);
   };
   if (t < T1) {
     {
-      uint4 va, vb;
-      issue(t, va, vb);
-      stash(t, va, vb);
-      issue(t + 1, va, vb);
-      stash(t + 1, va, vb);
+      uint4 va;
+      issue(t, va);
+      stash(t, va);
+      issue(t + 1, va);
+      stash(t + 1, va);
     }
     publish();
     if (l < 3) sm.b2s[w][l] = l == 0 ? b2_0 : l == 1 ? b2_1 : b2_2;

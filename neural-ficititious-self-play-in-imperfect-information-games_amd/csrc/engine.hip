@@ -582,7 +582,7 @@ int engine_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, bool own_streams, n
     EALLOC(L.br_perm, ueb);
     EALLOC(L.br_expl, sizeof(double) * 2 * L.umax);
     EALLOC(L.br_rec, sizeof(StepRec) * (ueb / CHAIN_MB));
-    EALLOC(L.ar_rec, sizeof(ArStepRec) * (ueb / CHAIN_MB));
+    EALLOC(L.ar_rec, sizeof(StepRec) * (ueb / CHAIN_MB));
     EALLOC(L.ar_active, 2 * L.umax);
     EALLOC(L.br_loss, 4 * 2 * L.umax * cfg->epochs);
     EALLOC(L.ar_loss, 4 * 2 * L.umax * cfg->epochs);

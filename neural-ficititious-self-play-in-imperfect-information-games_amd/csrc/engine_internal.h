@@ -108,27 +108,20 @@ struct Memories {
 // Everything one SGD step of a learner chain (learner.hip k_chain3) reads, built by the
 // prep kernels so the chain's lanes load their matrix-core operands directly:
 //   fa[g][s]  8 bf16 0/1 values: bits 4g..4g+3 and 16+4g..16+4g+3 of sample s's observation
-//             (the layer-1 K slots 8g..8g+7 of lane row g)
-//   ba[g][i]  the same bits of input i's 32-bit mask over the minibatch's 32 samples (the
-//             bit-transposed minibatch: the dW1 = X^T dZ1 operand)
-//   tg[s]     sample s's three fit targets and the step's lr
+//             (the layer-1 K slots 8g..8g+7 of lane row g), stored at fa[g][fa_slot(g, s)]
+//   tg[s]     sample s's three fit targets (AR: divided by the batch, exact) and the step's lr
+// 2,560 B per step.  The dW1 = X^T dZ1 operand (the bit-transposed minibatch) is not stored:
+// the chain reads it from the fa image in LDS with ds_read_b64_tr_b16 (chain3.h).  The chunks
+// of odd rows are XOR-swizzled (fa_slot), so the 16-byte row reads of the image are
+// conflict-free and the transposed reads 2-way (the minimum for 8-byte reads of one half of
+// each chunk).  AR: 1.21x the reference-layout bytes of its 32 sampled M_SL tuples (32 x
+// 132 B per epoch of two); BR: 0.62x (32 x 257 B).
 // Input 30 (CHAIN_BIAS_BIT) is the constant 1 of every sample: the chain keeps b1 as W1's
 // row 30, so the layer-1 products include the bias and dW1's row 30 is gb1.
 constexpr uint32_t CHAIN_BIAS_BIT = 1u << 30;
 constexpr int CHAIN_BIAS_IN = 30;
-struct __attribute__((aligned(16))) StepRec {      // the BR chain's record, 4,608 B
-  uint4 fa[4][32];
-  uint4 ba[4][32];
-  float4 tg[32];
-};
-// The AR chain's record, 2,560 B (1.21x the reference-layout bytes of its 32 sampled M_SL
-// tuples, 32 x 132 B per epoch of two).  It has no ba: the chain reads X^T from the fa image
-// in LDS with ds_read_b64_tr_b16.  Sample s of row g sits at fa[g][fa_slot(g, s)]: the chunks
-// of odd rows XOR-swizzled, so the 16-byte row reads of the image are conflict-free and the
-// transposed reads 2-way (the minimum for 8-byte reads of one half of each chunk).
-// tg[s]: sample s's three targets divided by the batch (exact) and the lr.
 __host__ __device__ constexpr int fa_slot(int g, int s) { return s ^ (12 * (g & 1)); }
-struct __attribute__((aligned(16))) ArStepRec {
+struct __attribute__((aligned(16))) StepRec {
   uint4 fa[4][32];
   float4 tg[32];
 };
@@ -145,7 +138,7 @@ struct LearnBufs {
   uint8_t* br_perm;    // [2][umax][epochs][batch]
   double* br_expl;     // [2][umax]
   StepRec* br_rec;     // [2][umax][epochs][batch / 32]: one record per SGD step
-  ArStepRec* ar_rec;   // [2][umax][epochs][batch / 32]
+  StepRec* ar_rec;     // [2][umax][epochs][batch / 32]
   float* br_loss;      // [2][umax][epochs] Keras epoch losses when the loss log is on (NaN:
   float* ar_loss;      //   no fit), the values agent/agent.py:243,264's TensorBoard logs
   uint8_t* ar_active;  // [2][umax]

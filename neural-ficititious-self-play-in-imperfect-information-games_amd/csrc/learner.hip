@@ -136,45 +136,15 @@ __device__ inline uint4 bits8u(uint32_t x, int g) {
                     ((n1 >> 2) & 1u) * 0x3F80u + ((n1 >> 3) & 1u) * 0x3F800000u);
 }
 
-// The BR chain records of one (update, epoch): the thread of fit position b holds its
-// observation mask x (for b < B), targets and the lr; minibatch b >> 5 gets fa / tg of its
-// sample b & 31, and ba from the bit transpose of its 32 masks by wave ballot.  Every valid
-// sample also carries the bias input (CHAIN_BIAS_BIT).  Called by whole waves whose lanes
-// hold positions b = 64 k + lane (k = 0, 1, ...: one record group of 64-thread waves).
+// The chain records of one (update, epoch): the thread of fit position b < B holds its
+// observation mask x, targets and the lr; minibatch b >> 5 gets the swizzled fa chunks and
+// tg of its sample b & 31 (the chain reads the transposed operand from fa itself).  Every
+// valid sample also carries the bias input (CHAIN_BIAS_BIT).
 __device__ inline void emit_recs(StepRec* __restrict__ recs, uint32_t x, float t0, float t1, float t2,
                                  float lr, int B, int b) {
   if (b < B) {
     x |= CHAIN_BIAS_BIT;
     StepRec& R = recs[b >> 5];
-    const int k = b & 31;
-#pragma unroll
-    for (int g = 0; g < 4; ++g) R.fa[g][k] = bits8u(x, g);
-    R.tg[k] = make_float4(t0, t1, t2, lr);
-  }
-  const int lane = b & 63;
-  unsigned long long mine = 0;
-#pragma unroll
-  for (int i = 0; i <= CHAIN_BIAS_IN; ++i) {
-    const unsigned long long m = __ballot((x >> i) & 1u);
-    if (lane == i) mine = m;
-  }
-  const int mb = (b >> 6) * 2;          // this wave's two minibatches
-  if (lane < 32) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      if (32 * (mb + h) >= B) continue;
-      const uint32_t xt = (uint32_t)(mine >> (32 * h));
-#pragma unroll
-      for (int g = 0; g < 4; ++g) recs[mb + h].ba[g][lane] = bits8u(xt, g);
-    }
-  }
-}
-// The AR chain's records (ArStepRec): the swizzled fa image and the targets (already / batch).
-__device__ inline void emit_ar_recs(ArStepRec* __restrict__ recs, uint32_t x, float t0, float t1, float t2,
-                                    float lr, int B, int b) {
-  if (b < B) {
-    x |= CHAIN_BIAS_BIT;
-    ArStepRec& R = recs[b >> 5];
     const int k = b & 31;
 #pragma unroll
     for (int g = 0; g < 4; ++g) R.fa[g][fa_slot(g, k)] = bits8u(x, g);
@@ -273,8 +243,8 @@ __global__ void __launch_bounds__(128) k_ar_prep(PrepArgs P0, const PrepArgs* __
     const bool in = b < P.B;
     // targets / batch: the AR chain's cross-entropy gradient takes them pre-scaled (exact)
     const float sc = 1.0f / (float)CHAIN_MB;
-    emit_ar_recs(P.LB.ar_rec + (slot_u * P.E + e) * (P.B / CHAIN_MB), in ? px[b] : 0u, in ? pt[b][0] * sc : 0.f,
-                 in ? pt[b][1] * sc : 0.f, in ? pt[b][2] * sc : 0.f, P.lr_ar, P.B, b);
+    emit_recs(P.LB.ar_rec + (slot_u * P.E + e) * (P.B / CHAIN_MB), in ? px[b] : 0u, in ? pt[b][0] * sc : 0.f,
+              in ? pt[b][1] * sc : 0.f, in ? pt[b][2] * sc : 0.f, P.lr_ar, P.B, b);
     __syncthreads();
   }
   if (last && b < P.B) P.M.dbg_rows[dbg * P.B + b] = cand[b];

@@ -71,33 +71,23 @@ int main(int argc, char** argv) {
   for (auto& v : w) v = ud(rng);
   for (int i = nn::OW2; i < nn::NP; ++i) w[i] *= wscale;
   // step records, as k_br_targets / k_ar_prep emit them
-  // BR: StepRec (targets and lr per sample); AR: ArStepRec (targets by output, / batch)
+  // step records as k_br_targets / k_ar_prep emit them (emit_recs): the swizzled fa image,
+  // targets (AR: / batch) and the lr per sample
   const size_t nrec = (size_t)U * E * NMB;
-  const size_t rsz = relu ? sizeof(StepRec) : sizeof(ArStepRec);
-  std::vector<StepRec> br_rec(relu ? nrec : 0);
-  std::vector<ArStepRec> ar_rec(relu ? 0 : nrec);
+  std::vector<StepRec> rec(nrec);
   for (size_t st = 0; st < nrec; ++st) {
     const int u = (int)(st / (E * NMB));
     const float lr = relu ? (float)(0.05 / (1.0 + 0.003 * sqrt((double)(2 * u)))) : 0.1f;
-    uint32_t xt[32] = {0};
     for (int k = 0; k < 32; ++k) {
       const auto& r = fit[st * 32 + k];
-      const uint32_t xb = r.x | CHAIN_BIAS_BIT;      // emit_recs: the bias input
-      if (relu) {
-        for (int g = 0; g < 4; ++g) br_rec[st].fa[g][k] = bits8_host(xb, g);
-        br_rec[st].tg[k] = make_float4(r.t0, r.t1, r.t2, lr);
-        for (int i = 0; i <= CHAIN_BIAS_IN; ++i) if ((xb >> i) & 1u) xt[i] |= 1u << k;
-      } else {                                      // emit_ar_recs: targets / batch
-        for (int g = 0; g < 4; ++g) ar_rec[st].fa[g][fa_slot(g, k)] = bits8_host(xb, g);
-        ar_rec[st].tg[k] = make_float4(r.t0 / 32.f, r.t1 / 32.f, r.t2 / 32.f, lr);
-      }
+      const uint32_t xb = r.x | CHAIN_BIAS_BIT;      // the bias input
+      for (int g = 0; g < 4; ++g) rec[st].fa[g][fa_slot(g, k)] = bits8_host(xb, g);
+      const float ts = relu ? 1.f : 1.f / 32.f;
+      rec[st].tg[k] = make_float4(r.t0 * ts, r.t1 * ts, r.t2 * ts, lr);
     }
-    if (relu)
-      for (int i = 0; i < 32; ++i)
-        for (int g = 0; g < 4; ++g) br_rec[st].ba[g][i] = bits8_host(xt[i], g);
   }
-  const void* rec_host = relu ? (const void*)br_rec.data() : (const void*)ar_rec.data();
-  const size_t rec_bytes = nrec * rsz;
+  const void* rec_host = rec.data();
+  const size_t rec_bytes = nrec * sizeof(StepRec);
   chainref::FitRow* dfit; char* drec; float* dw; unsigned long long* dst;
   CK(hipMalloc(&dfit, fit.size() * sizeof(chainref::FitRow)));
   CK(hipMalloc(&drec, rec_bytes));
@@ -111,7 +101,7 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&dw2, w.size() * 4));
   CK(hipMemcpy(dw2, w.data(), w.size() * 4, hipMemcpyHostToDevice));
   ChainArgs C{};
-  C.job[0].w = dw; C.job[0].rec = drec; C.job[0].u0 = 0; C.job[0].u1 = U; C.B = B; C.E = E; C.stamps = dst;
+  C.job[0].w = dw; C.job[0].rec = reinterpret_cast<const StepRec*>(drec); C.job[0].u0 = 0; C.job[0].u1 = U; C.B = B; C.E = E; C.stamps = dst;
   C.job[1] = C.job[0];
   C.job[1].w = dw2;                                  // second chain: same records, own weights
   chainref::RefArgs R{};
@@ -130,7 +120,7 @@ int main(int argc, char** argv) {
       CK(hipMemcpy(wall + (size_t)k * w.size(), w.data(), w.size() * 4, hipMemcpyHostToDevice));
       if (distinct) CK(hipMemcpy(rall + (size_t)k * rec_bytes, rec_host, rec_bytes, hipMemcpyHostToDevice));
       jobs[k].w = wall + (size_t)k * w.size();
-      jobs[k].rec = rall + (distinct ? (size_t)k * rec_bytes : 0);
+      jobs[k].rec = reinterpret_cast<const StepRec*>(rall + (distinct ? (size_t)k * rec_bytes : 0));
     }
     CK(hipMalloc(&djobs, sizeof(ChainJob) * nblk));
     CK(hipMemcpy(djobs, jobs.data(), sizeof(ChainJob) * nblk, hipMemcpyHostToDevice));
