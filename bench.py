@@ -501,10 +501,11 @@ def main():
         out = {"kernel": name, "bound": "issue", "achieved": issue, "peak": measured,
                "unit": "cycles per SGD step (static issue / measured)", "frac": issue / measured,
                "us_per_step": k_ms[name] * 1e3 / steps, "source": "profiles/r03_chain_census.json"}
-        pmc = os.path.join(REPO, "profiles", "r02_chain_pmc.json")   # tools/chain_pmc.sh
+        pmc = os.path.join(REPO, "profiles", "r03_chain_pmc.json")   # tools/chain_pmc.sh
         if os.path.exists(pmc):
             with open(pmc) as f:
                 out["sq_active_inst_frac"] = json.load(f)[net]["frac_active_inst"]
+            out["sq_source"] = "profiles/r03_chain_pmc.json"
         return out
     # the issue framing is per chain workgroup: the AR launch lasts as long as its longest
     # chain, a BR launch runs up to 2R segments side by side
