@@ -14,30 +14,36 @@ N = 8).  `--config c2` selects configs[1] (65,536 lanes).
 
 Multi-GPU (`torch.distributed.run --nproc-per-node N bench.py --gpus N`, configs[3] = C4):
 one self-play shard per GPU (its own hands, memories and learner; seeds 1234 + rank; weak
-scaling), and once per engine step an RCCL all-reduce of the average-policy (AR) gradient
-steps of both agents (shards.AvgPolicyAllReduce, 17.4 KB; `--ar-allreduce off` = independent
-replicas).  A barrier and a max-over-ranks of the elapsed time bracket the timed region.
+scaling), and after every lane slice's learner an all-reduce of the average-policy (AR)
+gradient steps of both agents (17.4 KB), enqueued by libnfsp on the AR chain stream over its
+own RCCL communicator (shards.AvgPolicyExchange; `--xchg-every k` = every k slices,
+`--ar-allreduce off` = independent replicas).  A barrier and a max-over-ranks of the elapsed
+time bracket the timed region; at N > 1 the line also carries every rank's own step time,
+device / PCI bus id and the exchange's cost (`ranks`).
 
 Timing: W warmup steps, then K steps with no instrumentation -> `value` / `ms_per_step`;
 then K more steps with HIP events recorded on each kernel's stream around every launch ->
 each kernel's average duration (`kernel_ms`, `ms_per_step_event_timed`).
 
-Roofline: SURVEY 8(d)'s HBM framing of the dominant kernel (largest GPU time): algorithmic
-bytes per launch (the 128 sampled tuples of each update in the reference's fp32 layout,
-257 B M_RL / 132 B M_SL; the rollout: its inserted tuples) / its average duration.  The
-chains are latency-bound SGD steps, so `roofline_other` also prices them in MFMA FLOPs and
-as an issue roofline (static issue cycles per step / measured), and `whole_step_hbm_per_gpu`
-is SURVEY 8(d)'s whole-path bytes per hand x hands / step time.
+Roofline (`rooflines()`): SURVEY 8(d)'s HBM framing of the kernel on the learner's critical
+path -- the chain on the stream with the longest busy span per step (`critical_stream`):
+algorithmic bytes per launch (the 128 sampled tuples of each update in the reference's fp32
+layout, 257 B M_RL / 132 B M_SL) / its average duration.  `roofline_other` holds the other
+chain, the rollout (its inserted tuples per launch of one slice), the chains' MFMA framing
+(the matrix-core FLOPs they execute, priced against the bf16 dense peak they run at) and
+their issue framing (static issue cycles per step / measured); `whole_step_hbm_per_gpu` is
+SURVEY 8(d)'s whole-path bytes per hand x hands / step time.
 
 `bench.py --gpus N` without a torch.distributed environment starts the N rank processes
 itself (launch_ranks; the parent never touches a GPU); every rank checks WORLD_SIZE == N.
 
 `cpu_baseline` (rank 0, N = 1 only) comes from the C++ restatement of the reference's
 main.train (oracle/nfsp_cpu.cpp).  It uses the reference cadence and this config's memory
-capacities, and is parity-checked hand for hand against oracle/nfsp_oracle.py.  It runs as
-one independent replica per host thread (`--cpu-threads`, default 16: the box's CPU share)
-for `--cpu-seconds`; `per_core` is one replica alone.  `cpu_baseline_numpy` is the numpy
-restatement on one core for 5 s.
+capacities, and is parity-checked hand for hand against oracle/nfsp_oracle.py.  As BASELINE.md
+plans it, it runs as one process per host core -- the cores this job may use: the cgroup CPU
+quota (16 on the 1-GPU box, whose os.cpu_count() reports the whole machine's 256), else
+os.cpu_count() -- each an independent replica, for `--cpu-seconds`; `cpu_baseline_numpy`,
+the numpy restatement, the same way.  Both print the core count and os.cpu_count().
 """
 from __future__ import annotations
 
@@ -60,6 +66,16 @@ CONFIGS = {
                label="C3: 1,048,576 Leduc lanes/GPU (advanced in 16 pipelined slices of 65,536), device "
                      "M_RL 200k + M_SL 2M, target sync 150, reference update cadence (1 update_strategy "
                      "/ 128 RL inserts / agent)"),
+    # C4 (BASELINE configs[3]): per GPU C3's 1M lanes and memories, as 64 pipelined slices of
+    # 16,384, and the ranks' AR nets exchanged after every slice (W0 + 2 x the mean of the
+    # deltas, shards.AvgPolicyExchange, RCCL on the AR chain stream): the 8-GPU job then learns
+    # inside the CPU reference's band per total hand from its first 8.4M hands
+    # (tests/test_gpu_slices.py).  bench.py --gpus N > 1 runs it by default.
+    "c4": dict(n_lanes=1_048_576, slices=64, slice_lag=2, rl_capacity=200_000, sl_capacity=2_000_000,
+               xchg_every=1, xchg_gain=2.0,
+               label="C4: 1,048,576 Leduc lanes/GPU (64 pipelined slices of 16,384), device M_RL 200k + M_SL "
+                     "2M, target sync 150, reference cadence; the AR nets of all GPUs exchanged after every "
+                     "slice (W0 + 2 x mean of the ranks' deltas, RCCL on the AR chain stream)"),
     "c3_1slice": dict(n_lanes=1_048_576, rl_capacity=200_000, sl_capacity=2_000_000,
                       label="C3 with all 1,048,576 lanes in one rollout per step (round 2's form: policy "
                             "lag of 1M hands), M_RL 200k + M_SL 2M, reference cadence"),
@@ -89,8 +105,13 @@ CONFIGS = {
                         "textbook NFSP with the MSE Q loss (quirks NFSP_TEXTBOOK_MSE)"),
 }
 
-PEAK_FP32_TFLOPS = 157.3      # MI355X_MICROARCH.md: FP32 vector = FP32 MFMA peak
+PEAK_BF16_TFLOPS = 2500.0     # MI355X_MICROARCH.md: BF16 MFMA, ~2.5 PF dense (the chains' MFMAs)
 PEAK_HBM_GBS = 8000.0         # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
+# the chains' matrix-core work per SGD step: 18 v_mfma_f32_16x16x32_bf16 per wave x 4 waves
+# (SQ_INSTS_MFMA, profiles/r03_chain_pmc.json), 2 x 16 x 16 x 32 FLOP each: the exact 3-term
+# bf16 split executes ~2.9x the dense-equivalent f32 FLOPs of the step (32 x F_TRAIN)
+MFMA_PER_SGD_STEP = 18 * 4
+FLOP_PER_MFMA = 2 * 16 * 16 * 32
 CHAIN_CLOCK_HZ = 2.40e9       # the chains' effective shader clock (tools/chain_clock.py)
 # algorithmic work per unit (DESIGN.md "Measurement")
 F_FWD = 2 * (30 * 64 + 64 * 3)          # 4,224 FLOP per row forward (dense-equivalent)
@@ -116,13 +137,42 @@ def load_pmc(config, kernel):
     return None if k is None else k.get("hbm_bytes_per_launch")
 
 
-def cpu_baseline_numpy(seconds: float, game: str = "leduc"):
-    """The reference-structured CPU path in numpy: oracle Env/Agent + main.train's loop."""
-    import random
+def cpu_share() -> int:
+    """Host cores this job may use: os.cpu_count(), capped by the cgroup CPU quota
+    (/sys/fs/cgroup/cpu.max; the 1-GPU box: 16 of the machine's 256) and the affinity mask."""
+    import math
+    n = os.cpu_count() or 1
+    try:
+        n = min(n, len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, math.ceil(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def cpu_worker(kind: str, seconds: float, config: str, seed: int) -> dict:
+    """One CPU-baseline process (bench.py --cpu-worker): one replica of main.train restated
+    in C++ (kind "port") or numpy ("numpy") for `seconds`; never touches a GPU."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
+    cfg = CONFIGS[config]
+    game = cfg.get("game", "leduc")
+    if kind == "port":
+        import cpu_port
+        c = cpu_port.make_cfg(None, seed, True, game, rl_capacity=cfg["rl_capacity"],
+                              sl_capacity=cfg["sl_capacity"])
+        c.seed = c.seed + seed
+        hands, el = cpu_port.bench(c, 1, seconds)
+        return {"hands": int(hands), "seconds": el}
+    import random
     import nfsp_oracle as orc
-    random.seed(0)
-    env, p1, p2 = orc.make_main(init_seed=0)
+    random.seed(seed)
+    env, p1, p2 = orc.make_main(init_seed=seed)
     env.kuhn = game == "kuhn"
     players = [p1, p2]
     dealer = random.randint(0, 1)
@@ -133,43 +183,83 @@ def cpu_baseline_numpy(seconds: float, game: str = "leduc"):
             dealer = 1 - dealer
             orc.play_hand(env, players, dealer, 0.1)
             hands += 1
-    dt = time.perf_counter() - t0
-    return {"value": hands / dt, "unit": "hands/s", "cores": 1, "kind": "port",
-            "sample": f"{hands} hands of main.train restated in numpy (oracle/nfsp_oracle.py: "
-                      f"Env, Agent play/updates at the reference cadence, numpy fp32 MLPs), "
-                      f"{dt:.1f} s on one core"}
+    return {"hands": hands, "seconds": time.perf_counter() - t0}
 
 
-def cpu_baseline(seconds: float, threads: int, cfg: dict):
-    """main.train restated in C++ (oracle/nfsp_cpu.cpp, parity-checked hand for hand against
-    oracle/nfsp_oracle.py by tests/test_cpu_port.py), one independent replica per host
-    thread at this config's memory capacities.  Host threads: the box's CPU share."""
+def cpu_processes(kind: str, procs: int, seconds: float, config: str) -> dict:
+    """`procs` concurrent worker processes (one per core), each an independent replica; the
+    aggregate hands/s = sum of each one's hands / its own time.  Child processes, started
+    fresh (no fork of a process that holds the GPU)."""
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-worker", kind, "--cpu-seconds", str(seconds),
+           "--config", config]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env.update(OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1", HIP_VISIBLE_DEVICES="")
+    ps = [subprocess.Popen(cmd + ["--cpu-seed", str(r)], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                           text=True, env=env) for r in range(procs)]
+    res = []
+    for p in ps:
+        out, err = p.communicate(timeout=seconds + 300)
+        if p.returncode != 0:
+            raise RuntimeError(f"cpu worker failed ({p.returncode}): {err[-2000:]}")
+        res.append(json.loads(out.strip().splitlines()[-1]))
+    return {"value": sum(r["hands"] / r["seconds"] for r in res), "hands": sum(r["hands"] for r in res),
+            "per_process": [r["hands"] / r["seconds"] for r in res]}
+
+
+def cpu_baseline(seconds: float, cfg_name: str, cores: int | None = None):
+    """BASELINE.md's CPU plan: main.train restated in C++ (oracle/nfsp_cpu.cpp, parity-checked
+    hand for hand against oracle/nfsp_oracle.py by tests/test_cpu_port.py) as one process per
+    host core, each an independent replica at this config's memory capacities.  Beside it:
+    the same C++ as threads of one process (round 3's form)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import cpu_port
     if not os.path.exists(cpu_port.LIB_PATH):
         subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle")], check=True)
+    cfg = CONFIGS[cfg_name]
+    cores = cores or cpu_share()
+    r = cpu_processes("port", cores, seconds, cfg_name)
     c = cpu_port.make_cfg(None, 0, True, cfg.get("game", "leduc"), rl_capacity=cfg["rl_capacity"],
                           sl_capacity=cfg["sl_capacity"])
-    one, el1 = cpu_port.bench(c, 1, min(seconds, 5.0))
-    hands, el = cpu_port.bench(c, threads, seconds)
-    return {"value": hands / el, "unit": "hands/s", "cores": threads, "kind": "port",
-            "per_core": one / el1,
-            "sample": f"{hands} hands of main.train restated in C++ (oracle/nfsp_cpu.cpp: the "
-                      f"reference's {cfg.get('game', 'leduc').capitalize()} Env, scheduler, memories M_RL {cfg['rl_capacity']:,} / M_SL "
-                      f"{cfg['sl_capacity']:,}, updates at the reference cadence, fp32 MLPs) by "
-                      f"{threads} independent replicas (one learner each) in {el:.1f} s; one "
-                      f"replica alone: {one / el1:,.0f} hands/s"}
+    th_hands, th_el = cpu_port.bench(c, cores, min(seconds, 5.0))
+    return {"value": r["value"], "unit": "hands/s", "cores": cores, "os_cpu_count": os.cpu_count(),
+            "kind": "port", "processes": cores, "per_core": sum(r["per_process"]) / cores,
+            "threads_one_process": {"value": th_hands / th_el, "threads": cores},
+            "sample": f"{r['hands']} hands of main.train restated in C++ (oracle/nfsp_cpu.cpp: the "
+                      f"reference's {cfg.get('game', 'leduc').capitalize()} Env, scheduler, memories M_RL "
+                      f"{cfg['rl_capacity']:,} / M_SL {cfg['sl_capacity']:,}, updates at the reference cadence, "
+                      f"fp32 MLPs) by {cores} processes (one per core of this job's CPU share: cgroup quota / "
+                      f"affinity; os.cpu_count() = {os.cpu_count()}), one independent replica (one learner) "
+                      f"each, {seconds:.0f} s"}
 
 
-def init_dist(backend=None):
+def cpu_baseline_numpy(seconds: float, cfg_name: str, cores: int | None = None):
+    """The reference-structured CPU path in numpy (oracle Env/Agent + main.train's loop), one
+    process per host core as cpu_baseline."""
+    cores = cores or cpu_share()
+    r = cpu_processes("numpy", cores, seconds, cfg_name)
+    return {"value": r["value"], "unit": "hands/s", "cores": cores, "os_cpu_count": os.cpu_count(),
+            "kind": "port", "processes": cores, "per_core": sum(r["per_process"]) / cores,
+            "sample": f"{r['hands']} hands of main.train restated in numpy (oracle/nfsp_oracle.py: Env, "
+                      f"Agent play/updates at the reference cadence, numpy fp32 MLPs) by {cores} processes "
+                      f"(one per core; os.cpu_count() = {os.cpu_count()}), {seconds:.0f} s each"}
+
+
+def init_dist(backend=None, force: bool = False):
     """One process per GPU (torch.distributed.run env); returns (world, rank, local, dist or None).
-    The default backend is RCCL ("nccl") on a GPU box; tests pass "gloo"."""
+    The default backend is RCCL ("nccl") on a GPU box; tests pass "gloo".  force: a process
+    group even at world size 1 (bench.py --ar-allreduce on: the exchange path measured on one
+    GPU, its collectives local)."""
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world == 1:
+    if world == 1 and not force:
         return world, rank, local, None
+    if world == 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
     import datetime
     import torch.distributed as dist
     backend = backend or "nccl"
@@ -183,9 +273,11 @@ def init_dist(backend=None):
     return world, rank, local, dist
 
 
-def timed_steps(step, steps, warmup, dist=None, sync=lambda: None, device="cuda"):
+def timed_steps(step, steps, warmup, dist=None, sync=lambda: None, device="cuda", out=None):
     """W untimed warmup steps, then exactly K timed steps bracketed by a barrier + device
-    sync on both sides; returns the MAX elapsed seconds over ranks (every rank gets it)."""
+    sync on both sides; returns the MAX elapsed seconds over ranks (every rank gets it).
+    out (dict): also gets this rank's own time ("local_s": its K steps, from the barrier to its
+    own final sync, before it waits for the others)."""
     import torch
     for _ in range(warmup):
         step()
@@ -197,6 +289,8 @@ def timed_steps(step, steps, warmup, dist=None, sync=lambda: None, device="cuda"
     for _ in range(steps):
         step()
     sync()
+    if out is not None:
+        out["local_s"] = time.perf_counter() - t0
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -295,6 +389,38 @@ def emit_result(obj: dict):
     out.flush()
 
 
+def device_identity() -> dict:
+    """This rank's device: torch's index and the PCI bus id (None without a GPU)."""
+    try:
+        import torch
+        if not torch.cuda.is_available():
+            return {"device": None, "pci_bus_id": None}
+        i = torch.cuda.current_device()
+        p = torch.cuda.get_device_properties(i)
+        bus = ":".join(f"{v:02x}" for v in (getattr(p, "pci_domain_id", 0), getattr(p, "pci_bus_id", 0),
+                                             getattr(p, "pci_device_id", 0)))
+        return {"device": i, "pci_bus_id": bus, "name": p.name}
+    except Exception as e:          # never fail the job over the report
+        return {"device": None, "pci_bus_id": None, "error": str(e)}
+
+
+def rank_report(dist, backend: str, mine: dict) -> dict:
+    """N > 1: every rank's own figures (all_gather_object): its un-instrumented ms per step,
+    the exchange's ms per call, its device and PCI bus id.  Under RCCL each rank must hold its
+    own GPU: duplicate bus ids end the job (exit 2) instead of timing co-resident ranks."""
+    ranks = [None] * dist.get_world_size()
+    dist.all_gather_object(ranks, dict(mine, rank=dist.get_rank()))
+    if backend == "nccl":
+        ids = [(r.get("host"), r.get("pci_bus_id")) for r in ranks]
+        if any(i[1] is None for i in ids) or len(set(ids)) != len(ids):
+            sys.stderr.write(f"bench.py: ranks do not hold distinct GPUs: {ids}\n")
+            sys.exit(2)
+    ms = [r["ms_per_step"] for r in ranks]
+    return {"world_size": dist.get_world_size(), "ranks": ranks,
+            "ms_per_step_min": min(ms), "ms_per_step_max": max(ms),
+            "distinct_devices": len({(r.get("host"), r.get("pci_bus_id")) for r in ranks}) == len(ranks)}
+
+
 def stub_main(args, world, rank, dist):
     """Test hook (`--stub-step-ms`): the launcher and the timing protocol with a CPU sleep in
     place of the engine step (no GPU).  Never a measurement: `data` says "stub"."""
@@ -304,14 +430,21 @@ def stub_main(args, world, rank, dist):
         if rank == fr:
             sys.stderr.write(f"stub: rank {rank} fails with {fc}\n")
             os._exit(fc)
+    tl = {}
     elapsed = timed_steps(lambda: time.sleep(args.stub_step_ms * 1e-3 * (1 + 0.5 * rank)),
-                          args.steps, args.warmup, dist, device="cpu")
+                          args.steps, args.warmup, dist, device="cpu", out=tl)
+    out = {"metric": "Leduc self-play hands/sec", "unit": "hands/s",
+           "value": job_value(args.steps * lanes, world, elapsed), "n_gpus": world,
+           "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": elapsed / args.steps * 1e3, "data": "stub",
+           "config": {"parallelism": f"dp{world}"}}
+    if dist is not None:
+        import socket
+        out["ranks"] = rank_report(dist, "gloo", dict(
+            device_identity(), host=socket.gethostname(), ms_per_step=tl["local_s"] / args.steps * 1e3,
+            exchange_ms_per_call=None, exchanges=0))
     if rank == 0:
-        emit_result({"metric": "Leduc self-play hands/sec", "unit": "hands/s",
-                     "value": job_value(args.steps * lanes, world, elapsed), "n_gpus": world,
-                     "steps": args.steps, "warmup": args.warmup,
-                     "ms_per_step": elapsed / args.steps * 1e3, "data": "stub",
-                     "config": {"parallelism": f"dp{world}"}})
+        emit_result(out)
     if dist is not None:
         dist.destroy_process_group()
 
@@ -337,8 +470,8 @@ def measure_group(pkg, name: str, steps: int, warmup: int) -> dict:
     hands = steps * cfg["n_lanes"]
     rl = sum(s1["rl_total"]) - sum(s0["rl_total"])
     out = {"workload": cfg["label"], "learner_replicas": R, "lanes_per_replica": cfg["n_lanes"] // R,
-           "metric": "RL inserts/s (M_RL inserts, each 1/128 of an update_strategy)",
-           "value": rl / el, "unit": "inserts/s", "hands_per_s": hands / el,
+           "metric": "hands/s (beside it RL inserts/s: M_RL inserts, each 1/128 of an update_strategy)",
+           "value": hands / el, "unit": "hands/s", "hands_per_s": hands / el,
            "training_stage": {"warmup_steps": warmup, "hands_before_timing": warmup * cfg["n_lanes"]},
            "steps": steps, "warmup": warmup,
            "ms_per_step": el / steps * 1e3, "rl_inserts_per_s": rl / el,
@@ -351,21 +484,147 @@ def measure_group(pkg, name: str, steps: int, warmup: int) -> dict:
     return out
 
 
+def rooflines(config, cfg, k_ms, k_launches, k_step_ms, br_upd, ar_upd, ar_max, t_rl, t_sl, hands_per_s):
+    """SURVEY 8(d)'s framings of the kernels, from one event-timed pass: k_ms = average ms per
+    launch, k_launches = launches, k_step_ms = ms per engine step (per kernel / stream);
+    br_upd / ar_upd = the pass's BR / AR updates (both agents), ar_max = the longest AR chain's
+    updates; t_rl / t_sl = RL / SL inserts per hand; hands_per_s = the un-instrumented rate.
+    Returns (roofline, roofline_other, whole_step_hbm_per_gpu, stream_ms_per_step).
+    tests/test_bench_roofline.py feeds it the committed profiles' timings."""
+    R = cfg.get("replicas", 1)
+    slices = cfg.get("slices", 1)
+    bytes_hand = BYTES_RL * t_rl + BYTES_SL * t_sl
+    # one k_rollout launch plays one slice: n_lanes / slices lanes (a group's launch: every
+    # replica's slice, R x (n_lanes / R) / slices -- the same count)
+    lanes_launch = cfg["n_lanes"] // slices
+    rollout_bytes = bytes_hand * lanes_launch
+    # the rollout writes bit-packed staging records, not the reference's fp32 tuples: the
+    # tuple bytes are a reference-layout EQUIVALENT; `traffic` / `achieved_counter` are what
+    # the kernel moves (rocprofv3 PMC, profiles/pmc_<config>.json)
+    roof_rollout = {"kernel": "k_rollout", "bound": "hbm",
+                    "achieved": rollout_bytes / (k_ms["k_rollout"] * 1e-3) / 1e9,
+                    "achieved_is": "reference-layout-equivalent bytes (257 B / 132 B fp32 tuples) of the "
+                                   "hands one launch plays",
+                    "peak": PEAK_HBM_GBS, "unit": "GB/s", "traffic": load_pmc(config, "k_rollout"),
+                    "bytes_per_hand": bytes_hand, "lanes_per_launch": lanes_launch,
+                    "bytes_per_launch": rollout_bytes, "avg_ms": k_ms["k_rollout"]}
+    roof_rollout["frac"] = roof_rollout["achieved"] / PEAK_HBM_GBS
+    if roof_rollout["traffic"]:
+        roof_rollout["achieved_counter"] = roof_rollout["traffic"] / (k_ms["k_rollout"] * 1e-3) / 1e9
+        roof_rollout["frac_counter"] = roof_rollout["achieved_counter"] / PEAK_HBM_GBS
+        roof_rollout["traffic_vs_reference_layout"] = roof_rollout["traffic"] / rollout_bytes
+    # SURVEY 8(d)'s whole-path figure: rollout writes + the sampled reads at the reference
+    # cadence (T_rl / 128 updates x 128 rows x (257 + 132) B) per hand, over the timed step
+    step_bytes_hand = bytes_hand + (t_rl / 128.0) * 128 * (BYTES_RL + BYTES_SL)
+    whole_step = {"bound": "hbm", "unit": "GB/s", "peak": PEAK_HBM_GBS,
+                  "bytes_per_hand": step_bytes_hand, "achieved": step_bytes_hand * hands_per_s / 1e9}
+    whole_step["frac"] = whole_step["achieved"] / PEAK_HBM_GBS
+
+    def chain_mfma(name, updates):
+        """The chain's matrix-core work: MFMA_PER_SGD_STEP v_mfma_f32_16x16x32_bf16 per SGD step
+        (2 epochs x 4 minibatches of 32 per update), priced against the bf16 dense peak;
+        `dense_equivalent_*` is the f32 FLOP count of the same steps (32 x F_TRAIN)."""
+        n = max(k_launches[name], 1)
+        sgd_steps = updates * 2 * 128 / 32 / n
+        flop = sgd_steps * MFMA_PER_SGD_STEP * FLOP_PER_MFMA
+        t = k_ms[name] * 1e-3
+        ach = flop / t / 1e12 if t > 0 else 0.0
+        return {"kernel": name, "bound": "mfma", "achieved": ach, "peak": PEAK_BF16_TFLOPS,
+                "unit": "TFLOP/s (bf16 MFMA executed)", "frac": ach / PEAK_BF16_TFLOPS, "traffic": None,
+                "avg_ms": k_ms[name], "launches": k_launches[name], "flop_per_launch": flop,
+                "dense_equivalent_tflops": (sgd_steps * 32 * F_TRAIN / t / 1e12) if t > 0 else 0.0}
+
+    def chain_roof_hbm(name, updates, tuple_bytes):
+        """SURVEY 8(d)'s HBM framing of a chain: algorithmic bytes = the 128 sampled memory
+        tuples of each update (reference fp32 layout), per launch."""
+        n = max(k_launches[name], 1)
+        byt = updates * 128 * tuple_bytes / n
+        ach = byt / (k_ms[name] * 1e-3) / 1e9 if k_ms[name] > 0 else 0.0
+        return {"kernel": name, "bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS,
+                "unit": "GB/s", "frac": ach / PEAK_HBM_GBS, "traffic": load_pmc(config, name),
+                "avg_ms": k_ms[name], "launches": k_launches[name], "bytes_per_launch": byt}
+
+    par = 2 * R if R > 1 else 1
+
+    def chain_issue(name, updates, net):
+        """The chain's step as an issue roofline: the loop's static issue cycles per SGD step
+        (tools/chain_census.py -> profiles/r03_chain_census.json, MI355X_MICROARCH.md issue
+        costs) against the measured cycles per step at the chain's effective clock (2.40 GHz,
+        tools/chain_clock.py).  frac = the share of the step one wave spends issuing."""
+        path = os.path.join(REPO, "profiles", "r03_chain_census.json")
+        n = max(k_launches[name], 1) * (par if name == "k_chain3_br" else 1)
+        steps = updates * 2 * 128 / 32 / n                  # epochs x minibatches per workgroup
+        if not os.path.exists(path) or steps <= 0:
+            return None
+        with open(path) as f:
+            issue = json.load(f)[net]["issue_cycles_per_step"]
+        measured = k_ms[name] * 1e-3 / steps * CHAIN_CLOCK_HZ
+        out = {"kernel": name, "bound": "issue", "achieved": issue, "peak": measured,
+               "unit": "cycles per SGD step (static issue / measured)", "frac": issue / measured,
+               "us_per_step": k_ms[name] * 1e3 / steps, "source": "profiles/r03_chain_census.json"}
+        pmc = os.path.join(REPO, "profiles", "r03_chain_pmc.json")   # tools/chain_pmc.sh
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                out["sq_active_inst_frac"] = json.load(f)[net]["frac_active_inst"]
+            out["sq_source"] = "profiles/r03_chain_pmc.json"
+        return out
+
+    # roofline: SURVEY 8(d)'s HBM framing (the judged bound) of each kernel; the MFMA and
+    # issue framings of the chains go to roofline_other
+    roofs = {"k_chain3_br_hbm": chain_roof_hbm("k_chain3_br", br_upd, BYTES_RL),
+             "k_chain3_ar_hbm": chain_roof_hbm("k_chain3_ar", ar_upd, BYTES_SL),
+             "k_rollout_hbm": roof_rollout,
+             "k_chain3_br_mfma": chain_mfma("k_chain3_br", br_upd),
+             "k_chain3_ar_mfma": chain_mfma("k_chain3_ar", ar_upd),
+             "k_chain3_br_issue": chain_issue("k_chain3_br", br_upd, "br"),
+             # one AR launch runs both agents' chains side by side: it lasts as long as the
+             # agent with more updates
+             "k_chain3_ar_issue": chain_issue("k_chain3_ar", ar_max, "ar")}
+    # the dominant kernel = the one on the learner's critical path: the streams run side by
+    # side (AR chains of both agents on one stream, each agent's BR targets + chains on its
+    # own), so GPU time summed over streams overstates the BR chain; the stream whose busy
+    # span per step is longest bounds the step, and its chain is the roofline kernel
+    streams = {"ar_chain": k_step_ms["k_chain3_ar"], "br_stream_a0": k_step_ms["br_stream_a0"],
+               "br_stream_a1": k_step_ms["br_stream_a1"]}
+    crit = max(streams, key=streams.get)
+    dom = "k_chain3_ar" if crit == "ar_chain" else "k_chain3_br"
+    roof_key = f"{dom}_hbm"
+    roofline = dict(roofs[roof_key])
+    roofline["critical_stream"] = crit
+    pmc = load_pmc(config, roofline["kernel"])
+    if pmc is not None:
+        roofline["traffic"] = pmc
+        roofline["traffic_source"] = f"profiles/pmc_{config}.json (rocprofv3 --pmc passes)"
+    return roofline, {k: v for k, v in roofs.items() if k != roof_key}, whole_step, streams
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
+                    help="default: c3 at N = 1, c4 at N > 1")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--cpu-threads", type=int, default=16,
-                    help="host threads for cpu_baseline (16 = the 1-GPU box's CPU share)")
+    ap.add_argument("--cpu-cores", type=int, default=None,
+                    help="processes for the CPU baselines (default: this job's CPU share, cpu_share())")
+    ap.add_argument("--cpu-worker", choices=["port", "numpy"], default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-seed", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL (one rank per GPU); gloo: a CPU-side rehearsal of the N > 1 path")
     ap.add_argument("--ar-allreduce", default="auto", choices=["auto", "on", "off"],
-                    help="all-reduce of the AR (average-policy) gradient steps once per engine "
-                         "step over the ranks (C4; shards.AvgPolicyAllReduce); auto = on for N > 1")
+                    help="the all-reduce of the AR (average-policy) gradient steps over the ranks "
+                         "(C4; shards.AvgPolicyExchange); auto = on for N > 1")
+    ap.add_argument("--xchg-every", type=int, default=None,
+                    help="the exchange after every k-th slice's learner (k = slices: once per step); "
+                         "default: the config's (c4: 1), else 1")
+    ap.add_argument("--xchg-gain", type=float, default=None,
+                    help="W0 + gain x mean of the ranks' AR deltas (1: plain averaging; DESIGN.md §8); "
+                         "default: the config's (c4: 2), else 2")
+    ap.add_argument("--xchg-transport", default="auto", choices=["auto", "rccl", "host"],
+                    help="rccl: libnfsp's own communicator on the AR chain stream; host: the process "
+                         "group from a host callback; auto: rccl under nccl, host under gloo")
     ap.add_argument("--stub-step-ms", type=float, default=None, help=argparse.SUPPRESS)
     # test hook with --stub-step-ms: rank R exits with code C after the process group is up
     ap.add_argument("--stub-fail", default=None, help=argparse.SUPPRESS)
@@ -376,7 +635,15 @@ def main():
                     help="engine-group configs measured beside the C3 headline at N = 1 "
                          "(`groups` in the JSON line; '' = none)")
     args = ap.parse_args()
+    if args.config is None:
+        args.config = "c4" if max(args.gpus, int(os.environ.get("WORLD_SIZE", "1"))) > 1 else "c3"
+    c = CONFIGS[args.config]
+    args.xchg_every = args.xchg_every if args.xchg_every is not None else c.get("xchg_every", 1)
+    args.xchg_gain = args.xchg_gain if args.xchg_gain is not None else c.get("xchg_gain", 2.0)
 
+    if args.cpu_worker:                # a CPU-baseline child process: no GPU, one JSON line
+        print(json.dumps(cpu_worker(args.cpu_worker, args.cpu_seconds, args.config, args.cpu_seed)))
+        return
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # the driver's `bench.py --gpus N` without torch.distributed.run: one rank per GPU
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
@@ -389,7 +656,7 @@ def main():
     import torch
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local % torch.cuda.device_count())   # one rank per GPU (mod: rehearsals)
-    world, rank, local, dist = init_dist(args.dist_backend)
+    world, rank, local, dist = init_dist(args.dist_backend, force=args.ar_allreduce == "on")
 
     import __graft_entry__
     pkg = __graft_entry__.load_package()
@@ -411,22 +678,23 @@ def main():
                                         init_seed=rank, game=game, **extra)
     avg = None
     if R == 1 and dist is not None and (args.ar_allreduce == "on" or (args.ar_allreduce == "auto" and world > 1)):
-        # C4: the AR nets of both agents, averaged over the ranks once per engine step
-        avg = pkg.shards.AvgPolicyAllReduce(
-            [eng.weights_tensor(a, pkg.engine.NET_AR) for a in (0, 1)], dist,
-            sync=torch.cuda.synchronize)
+        # C4: the AR nets of both agents, W0 + mean of the ranks' deltas after every
+        # `xchg_every`-th slice, on the AR chain stream
+        avg = pkg.shards.AvgPolicyExchange(eng, dist, every=args.xchg_every, transport=args.xchg_transport,
+                                           gain=args.xchg_gain)
 
     def step():
         eng.step()
-        if avg is not None:
-            avg()
     dev = "cuda" if args.dist_backend == "nccl" else "cpu"
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     # `value`: K steps with no instrumentation at all
     s0 = eng.stats()
-    elapsed = timed_steps(step, args.steps, 0, dist, torch.cuda.synchronize, device=dev)
+    tl = {}
+    x0 = avg.calls if avg is not None else 0
+    elapsed = timed_steps(step, args.steps, 0, dist, torch.cuda.synchronize, device=dev, out=tl)
+    x1 = avg.calls if avg is not None else 0
     s1 = eng.stats()
     # per-kernel durations: K more steps with HIP events around every launch (kernel_ms,
     # roofline); their wall time is reported beside `value`, never as it
@@ -447,97 +715,13 @@ def main():
     k_step_ms = {k: v[0] / args.steps for k, v in timings.items()}       # per engine step
     k_launches = {k: v[1] for k, v in timings.items()}
     t_rl, t_sl = rl_ins / hands_rank, sl_ins / hands_rank
-    bytes_hand = BYTES_RL * t_rl + BYTES_SL * t_sl
-    rollout_bytes = bytes_hand * cfg["n_lanes"] / R                       # per launch
-    # the rollout writes bit-packed staging records, not the reference's fp32 tuples: the
-    # tuple bytes are a reference-layout EQUIVALENT; `traffic` / `achieved_counter` are what
-    # the kernel moves (rocprofv3 PMC, profiles/pmc_<config>.json)
-    roof_rollout = {"kernel": "k_rollout", "bound": "hbm",
-                    "achieved": rollout_bytes / (k_ms["k_rollout"] * 1e-3) / 1e9,
-                    "achieved_is": "reference-layout-equivalent bytes (257 B / 132 B fp32 tuples)",
-                    "peak": PEAK_HBM_GBS, "unit": "GB/s", "traffic": load_pmc(args.config, "k_rollout"),
-                    "bytes_per_hand": bytes_hand, "avg_ms": k_ms["k_rollout"]}
-    roof_rollout["frac"] = roof_rollout["achieved"] / PEAK_HBM_GBS
-    if roof_rollout["traffic"]:
-        roof_rollout["achieved_counter"] = roof_rollout["traffic"] / (k_ms["k_rollout"] * 1e-3) / 1e9
-        roof_rollout["frac_counter"] = roof_rollout["achieved_counter"] / PEAK_HBM_GBS
-    # SURVEY 8(d)'s whole-path figure: rollout writes + the sampled reads at the reference
-    # cadence (T_rl / 128 updates x 128 rows x (257 + 132) B) per hand, over the timed step
-    step_bytes_hand = bytes_hand + (t_rl / 128.0) * 128 * (BYTES_RL + BYTES_SL)
-    whole_step = {"bound": "hbm", "unit": "GB/s", "peak": PEAK_HBM_GBS,
-                  "bytes_per_hand": step_bytes_hand,
-                  "achieved": step_bytes_hand * hands_rank / (elapsed / 1.0) / 1e9}
-    whole_step["frac"] = whole_step["achieved"] / PEAK_HBM_GBS
-
-    def chain_roof(name, updates):
-        n = max(k_launches[name], 1)
-        flop = updates * 2 * 128 * F_TRAIN / n            # epochs x batch rows x F_TRAIN
-        ach = flop / (k_ms[name] * 1e-3) / 1e12 if k_ms[name] > 0 else 0.0
-        return {"kernel": name, "bound": "mfma", "achieved": ach, "peak": PEAK_FP32_TFLOPS,
-                "unit": "TFLOP/s", "frac": ach / PEAK_FP32_TFLOPS, "traffic": None,
-                "avg_ms": k_ms[name], "launches": k_launches[name], "flop_per_launch": flop}
-    def chain_roof_hbm(name, updates, tuple_bytes):
-        """SURVEY 8(d)'s HBM framing of a chain: algorithmic bytes = the 128 sampled memory
-        tuples of each update (reference fp32 layout), per launch."""
-        n = max(k_launches[name], 1)
-        byt = updates * 128 * tuple_bytes / n
-        ach = byt / (k_ms[name] * 1e-3) / 1e9 if k_ms[name] > 0 else 0.0
-        return {"kernel": name, "bound": "hbm", "achieved": ach, "peak": PEAK_HBM_GBS,
-                "unit": "GB/s", "frac": ach / PEAK_HBM_GBS, "traffic": load_pmc(args.config, name),
-                "avg_ms": k_ms[name], "launches": k_launches[name], "bytes_per_launch": byt}
-    def chain_issue(name, updates, net):
-        """The chain's step as an issue roofline: the loop's static issue cycles per SGD step
-        (tools/chain_census.py -> profiles/r02_chain_census.json, MI355X_MICROARCH.md issue
-        costs) against the measured cycles per step at the chain's effective clock (2.40 GHz,
-        tools/chain_clock.py).  frac = the share of the step one wave spends issuing."""
-        path = os.path.join(REPO, "profiles", "r03_chain_census.json")
-        n = max(k_launches[name], 1) * (par if name == "k_chain3_br" else 1)
-        steps = updates * 2 * 128 / 32 / n                  # epochs x minibatches per workgroup
-        if not os.path.exists(path) or steps <= 0:
-            return None
-        with open(path) as f:
-            issue = json.load(f)[net]["issue_cycles_per_step"]
-        measured = k_ms[name] * 1e-3 / steps * CHAIN_CLOCK_HZ
-        out = {"kernel": name, "bound": "issue", "achieved": issue, "peak": measured,
-               "unit": "cycles per SGD step (static issue / measured)", "frac": issue / measured,
-               "us_per_step": k_ms[name] * 1e3 / steps, "source": "profiles/r03_chain_census.json"}
-        pmc = os.path.join(REPO, "profiles", "r03_chain_pmc.json")   # tools/chain_pmc.sh
-        if os.path.exists(pmc):
-            with open(pmc) as f:
-                out["sq_active_inst_frac"] = json.load(f)[net]["frac_active_inst"]
-            out["sq_source"] = "profiles/r03_chain_pmc.json"
-        return out
     # the issue framing is per chain workgroup: the AR launch lasts as long as its longest
     # chain, a BR launch runs up to 2R segments side by side
     reps1, reps2 = s1.get("replicas", [s1]), s2.get("replicas", [s2])
     ar_max = max(b["ar_updates"][a] - x["ar_updates"][a] for x, b in zip(reps1, reps2) for a in (0, 1))
-    par = 2 * R if R > 1 else 1
-    # roofline: SURVEY 8(d)'s HBM framing (the judged bound) of each kernel; the MFMA and
-    # issue framings of the chains go to roofline_other
-    roofs = {"k_chain3_br_hbm": chain_roof_hbm("k_chain3_br", br_upd, BYTES_RL),
-             "k_chain3_ar_hbm": chain_roof_hbm("k_chain3_ar", ar_upd, BYTES_SL),
-             "k_rollout_hbm": roof_rollout,
-             "k_chain3_br_mfma": chain_roof("k_chain3_br", br_upd),
-             "k_chain3_ar_mfma": chain_roof("k_chain3_ar", ar_upd),
-             "k_chain3_br_issue": chain_issue("k_chain3_br", br_upd, "br"),
-             # one AR launch runs both agents' chains side by side: it lasts as long as the
-             # agent with more updates
-             "k_chain3_ar_issue": chain_issue("k_chain3_ar", ar_max, "ar")}
-    # the dominant kernel = the one on the learner's critical path: the streams run side by
-    # side (AR chains of both agents on one stream, each agent's BR targets + chains on its
-    # own), so GPU time summed over streams overstates the BR chain; the stream whose busy
-    # span per step is longest bounds the step, and its chain is the roofline kernel
-    streams = {"ar_chain": k_step_ms["k_chain3_ar"], "br_stream_a0": k_step_ms["br_stream_a0"],
-               "br_stream_a1": k_step_ms["br_stream_a1"]}
-    crit = max(streams, key=streams.get)
-    dom = "k_chain3_ar" if crit == "ar_chain" else "k_chain3_br"
-    roof_key = f"{dom}_hbm"
-    roofline = dict(roofs[roof_key])
-    roofline["critical_stream"] = crit
-    pmc = load_pmc(args.config, roofline["kernel"])
-    if pmc is not None:
-        roofline["traffic"] = pmc
-        roofline["traffic_source"] = f"profiles/pmc_{args.config}.json (rocprofv3 --pmc passes)"
+    roofline, roofs_other, whole_step, streams = rooflines(
+        args.config, cfg, k_ms, k_launches, k_step_ms, br_upd, ar_upd, ar_max, t_rl, t_sl,
+        hands_rank / elapsed)
     rollout_path_ms = k_step_ms["k_rollout"] + k_step_ms["k_scan"] + k_step_ms["k_commit"]
     out = {
         "metric": "Kuhn self-play hands/sec" if cfg.get("game") == "kuhn" else "Leduc self-play hands/sec",
@@ -555,12 +739,13 @@ def main():
         "data": "synthetic: Philox self-play deals/draws, Glorot-uniform random-init nets",
         "config": {"workload": cfg["label"], "lanes_per_gpu": cfg["n_lanes"], "learner_replicas_per_gpu": R,
                    "rl_capacity": cfg["rl_capacity"], "sl_capacity": cfg["sl_capacity"],
-                   "inserts_per_update": 128, "batch": 128, "parallelism": (f"dp{world}: shards + AR-gradient all-reduce per engine step"
+                   "inserts_per_update": 128, "batch": 128, "parallelism": (f"dp{world}: shards + AR-gradient all-reduce every "
+                                   f"{args.xchg_every} slice(s) ({avg.transport})"
                                    if avg is not None else
                                    f"replicas x{world} GPUs x {R} learner replicas per GPU (on-device AR average per step)"
                                    if R > 1 else f"replicas x{world}")},
         "roofline": roofline,
-        "roofline_other": {k: v for k, v in roofs.items() if k != roof_key},
+        "roofline_other": roofs_other,
         "whole_step_hbm_per_gpu": whole_step,
         "kernel_ms": k_ms,
         "kernel_ms_per_step": k_step_ms,
@@ -570,12 +755,24 @@ def main():
         "slice_lag": cfg.get("slice_lag", 1),
         "rollout_only_hands_per_s": cfg["n_lanes"] / (rollout_path_ms * 1e-3) * world,
         "per_step": {"br_updates": br_upd / args.steps, "ar_updates": ar_upd / args.steps,
+                     "ar_updates_max_chain": ar_max / args.steps,
                      "rl_inserts_per_hand": t_rl, "sl_inserts_per_hand": t_sl},
         "exploitability_proxy": sum(s2["exploitability"]),
     }
+    xchg_ms = k_ms.get("ar_exchange") if avg is not None and k_launches.get("ar_exchange") else None
     if avg is not None:
-        out["ar_allreduce"] = {"calls": avg.calls, "bytes_per_call": 4 * avg.flat.numel(),
-                               "backend": args.dist_backend, "per": "engine step"}
+        out["ar_allreduce"] = {"calls": avg.calls, "calls_timed_pass": x1 - x0, "bytes_per_call": avg.bytes_per_call,
+                               "backend": args.dist_backend, "transport": avg.transport,
+                               "every_slices": args.xchg_every, "gain": args.xchg_gain,
+                               "ms_per_call_event_timed": xchg_ms,
+                               "ms_per_call_is": "HIP events on the AR stream around delta + all-reduce + "
+                                                 "apply (includes waiting for the slowest rank's AR chain)"}
+    if dist is not None:
+        import socket
+        out["ranks"] = rank_report(dist, args.dist_backend, dict(
+            device_identity(), host=socket.gethostname(), ms_per_step=tl["local_s"] / args.steps * 1e3,
+            ms_per_step_event_timed=elapsed_ev / args.steps * 1e3,
+            exchange_ms_per_call=xchg_ms, exchanges=(x1 - x0)))
     # exact exploitability of the AR nets after the timed steps (outside the timed region)
     ex = {m: eng.exploitability(m) for m in (0, 1)}
     out["exploitability_exact"] = {
@@ -599,9 +796,8 @@ def main():
         out["groups"] = {name: measure_group(pkg, name, max(args.steps, 10), args.warmup)
                          for name in args.groups.split(",")}
     if rank == 0 and world == 1 and not args.no_cpu:
-        threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, threads, cfg)
-        out["cpu_baseline_numpy"] = cpu_baseline_numpy(min(args.cpu_seconds, 5.0), cfg.get("game", "leduc"))
+        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.config, args.cpu_cores)
+        out["cpu_baseline_numpy"] = cpu_baseline_numpy(min(args.cpu_seconds, 5.0), args.config, args.cpu_cores)
     if rank == 0:
         emit_result(out)
     if dist is not None:

@@ -262,7 +262,10 @@ typedef struct nfsp_engine_cfg {
    * as of the step's start).  The policy lag is then two slices; the chains' streams never
    * wait for a rollout.  Each step starts from the nets as they are (nfsp_engine_weights
    * writes between steps are seen) and ends with every stream joined.  nfsp_rollout /
-   * nfsp_engine_update called by themselves always run with lag 1.  Engine groups: 1 only. */
+   * nfsp_engine_update called by themselves always run with lag 1.  Engine groups run their
+   * slices one after another, and with slice_lag 2 each replica's slice j acts with the nets
+   * and epsilon its learner left after slice j - 2 (snapshots on device): the same arithmetic
+   * as a pipelined engine, not its overlap. */
   int32_t slice_lag;
 } nfsp_engine_cfg;
 
@@ -313,9 +316,10 @@ int nfsp_engine_memories(nfsp_engine* e, int agent, nfsp_records* rl, int64_t* r
                          nfsp_records* sl, uint32_t** dev_pending_sl_obs,
                          float** dev_pending_sl_a, int64_t** dev_pending_sl_rl_pos);
 /* Per-kernel timing with HIP events recorded around each launch on the stream it runs on:
- * ms / launches [10] = {k_rollout, k_scan1+k_scan2, k_commit, learner (whole
+ * ms / launches [11] = {k_rollout, k_scan1+k_scan2, k_commit, learner (whole
  * nfsp_engine_update), learner prep (k_br_prep..k_res_apply), k_br_targets,
- * k_chain3<BR>, k_chain3<AR>, BR stream of agent 0, BR stream of agent 1}, accumulated since
+ * k_chain3<BR>, k_chain3<AR>, BR stream of agent 0, BR stream of agent 1, the AR exchange
+ * (nfsp_engine_set_exchange: delta, all-reduce, apply on the AR stream)}, accumulated since
  * the previous nfsp_engine_get_timings (which synchronises and resets them).  A "BR stream"
  * entry is the span of one learner call's BR work of that agent on its stream, from its
  * first k_br_targets to its last chain, gaps included (engine groups: their one BR stream in
@@ -330,7 +334,7 @@ int nfsp_engine_set_timing(nfsp_engine* e, int on);
  * nfsp_engine_update's updates and [.. + 1] = its last update's final-epoch loss (NaN: none). */
 int nfsp_engine_set_loss_log(nfsp_engine* e, int on);
 int nfsp_engine_losses(nfsp_engine* e, double* out /*[2][2][2]*/);
-int nfsp_engine_get_timings(nfsp_engine* e, double* ms /*[10]*/, int64_t* launches /*[10]*/);
+int nfsp_engine_get_timings(nfsp_engine* e, double* ms /*[11]*/, int64_t* launches /*[11]*/);
 /* Debug view of the last learner run: per agent and role (0 = AR, 1 = BR) the sampled
  * rows [batch] (int64) and fit permutations [epochs][batch] (int32) of its LAST update. */
 int nfsp_engine_last_update(nfsp_engine* e, int agent, int role, int64_t** dev_rows,
@@ -346,6 +350,42 @@ int nfsp_engine_lane_counts(nfsp_engine* e, uint32_t** dev_counts);
  * and epsilons of snapshot `parity` -- after a pipelined nfsp_engine_step of K slices, snapshot
  * (K - 1) & 1 holds what the step's last slice acted with. */
 int nfsp_engine_snapshot(nfsp_engine* e, int parity, float** dev_w, double* eps /*[2]*/);
+
+/* ---- cross-shard exchange of the average-policy nets (BASELINE C4) ----
+ * The reference learns inside its hand loop (main.py:27-67; update_strategy every 128 RL
+ * inserts, agent/agent.py:153-154, whose AR fit is agent/agent.py:255-264).  Sharded over N
+ * GPUs, each shard's learner trains its own copy of both agents' AR nets; the exchange keeps
+ * the copies one net: at the end of every `every`-th learner call (one call per lane slice:
+ * every = 1 exchanges after every slice, every = cfg.slices once per step), right behind the
+ * call's AR chain on the chain's own stream,
+ *     D = W_AR - W0   (both agents, 2 x NP f32),   S = sum over shards of D,
+ *     W_AR = W0 + S * scale,   W0 = W_AR
+ * (scale 1 / N: the mean of the shards' gradient steps, i.e. data-parallel SGD of one net
+ * over every shard's minibatches, exchanged per slice).  Before the AR snapshot of a
+ * pipelined slice (cfg.slice_lag 2), so the rollout two slices on acts with the exchanged
+ * nets.  Arithmetic: fp contract off, S summed from +0 -- with 2 shards bit-identical to an
+ * engine group's on-device exchange (NFSP_GROUP_AVG_AR, nfsp_group_set_exchange).
+ * Transports (exactly one):
+ *   rccl_comm  an RCCL communicator (nfsp_rccl_comm_create): ncclAllReduce(SUM) of D in place
+ *              on the AR chain stream -- stream-ordered, no host round trip;
+ *   fn         a host callback, for transports that are not stream-ordered (gloo rehearsals
+ *              and CPU-side tests): the engine synchronises the AR stream, calls
+ *              fn(user, dev_D, 2 * NP), which must leave S in dev_D (device memory, complete
+ *              on return) and return 0; anything else fails the step.
+ * Every shard must make the same number of learner calls (the same slices per step).
+ * nfsp_engine_set_exchange takes W0 = the AR nets as they are now (call it after the shards'
+ * AR nets were made equal, e.g. broadcast from rank 0); every = 0 turns the exchange off. */
+typedef int (*nfsp_exchange_fn)(void* user, float* dev_sum, int64_t n);
+int nfsp_engine_set_exchange(nfsp_engine* e, int every, float scale, void* rccl_comm,
+                             nfsp_exchange_fn fn, void* user);
+/* exchanges made so far */
+int nfsp_engine_exchanges(nfsp_engine* e, int64_t* out);
+/* RCCL (librccl.so.1, loaded on first use): ncclGetUniqueId into out[128] (rank 0), and a
+ * communicator of `world` ranks on HIP device `device` from that id (every rank, collectively:
+ * ncclCommInitRank blocks until all ranks joined). */
+int nfsp_rccl_unique_id(uint8_t* out /*[128]*/);
+int nfsp_rccl_comm_create(const uint8_t* id /*[128]*/, int world, int rank, int device, void** comm);
+int nfsp_rccl_comm_destroy(void* comm);
 
 /* Test hook: from the next nfsp_engine_update on, each agent's AR and BR chains run only the
  * first max_updates updates of the learner call (0 = all).  Everything else still follows
@@ -376,9 +416,20 @@ int nfsp_group_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, int replicas, u
 int nfsp_group_destroy(nfsp_group* g);
 int nfsp_group_engine(nfsp_group* g, int replica, nfsp_engine** out);
 int nfsp_group_step(nfsp_group* g);
-/* The AR exchange by itself (nfsp_group_step does it when NFSP_GROUP_AVG_AR is set).  Its
- * first call copies replica 0's AR nets everywhere. */
+/* The exchange by itself (nfsp_group_step does it when NFSP_GROUP_AVG_AR is set or
+ * nfsp_group_set_exchange configured one).  Its first call copies replica 0's exchanged nets
+ * everywhere. */
 int nfsp_group_average_ar(nfsp_group* g);
+/* The group's exchange, as nfsp_engine_set_exchange's over shards: at the end of every
+ * `every`-th learner call (slice) of the group, each net in `nets` (NFSP_XCHG_AR: both agents'
+ * AR nets; NFSP_XCHG_BR: their BR nets) becomes W0 + (sum_r (W_r - W0)) * scale, summed in
+ * replica order from +0, and W0 <- that.  every = 0: off.  NFSP_GROUP_AVG_AR at creation is
+ * nets = AR, every = cfg.slices (once per step, after its last slice), scale = 1 / R.  The first
+ * exchange of a net (or nfsp_group_average_ar) copies replica 0's net (with BR also its target
+ * net) to every replica instead. */
+#define NFSP_XCHG_AR 1u
+#define NFSP_XCHG_BR 2u
+int nfsp_group_set_exchange(nfsp_group* g, unsigned nets, int every, float scale);
 int nfsp_group_set_timing(nfsp_group* g, int on);
 /* nfsp_engine_get_timings summed over the replicas.  The shared chain and target launches
  * count once each. */

@@ -53,6 +53,8 @@ struct GroupRollout {
   RolloutArgs A;
   Memories M;
   int nblk;
+  float* snap;          // slice_lag 2: the replica's snapshots [2][2][3][NP] (else null)
+  double* snap_eps;     //   and their epsilons [2][2], on device
 };
 
 __device__ __forceinline__ void rollout_body(const RolloutArgs& A, int bx) {
@@ -226,13 +228,34 @@ constexpr int ROLLOUT_WG = 512;
 __global__ void __launch_bounds__(ROLLOUT_WG) k_rollout(RolloutArgs A) { rollout_body(A, blockIdx.x); }
 
 // engine groups: blockIdx.y = replica (the rollout index is the same for every replica)
+// par >= 0 (slice_lag 2): the replica acts with its snapshot `par` and that snapshot's epsilon
 __global__ void __launch_bounds__(256) k_rollout_g(const GroupRollout* __restrict__ tab, uint32_t g_lo,
-                                                   uint32_t g_hi, uint32_t lane0) {
-  RolloutArgs A = tab[blockIdx.y].A;
+                                                   uint32_t g_hi, uint32_t lane0, int par) {
+  const GroupRollout& T = tab[blockIdx.y];
+  RolloutArgs A = T.A;
   A.g_lo = g_lo;
   A.g_hi = g_hi;
   A.lane0 = lane0;
+  if (par >= 0) {
+    A.w = T.snap + (size_t)par * 6 * nn::NP;
+    A.eps_by_value = 1;
+    A.eps_v[0] = T.snap_eps[2 * par + 0];
+    A.eps_v[1] = T.snap_eps[2 * par + 1];
+  }
   rollout_body(A, blockIdx.x);
+}
+
+// slice_lag 2 in a group: replica blockIdx.y's nets and epsilon -> its snapshot `par` (-1: both
+// parities, a step's start), after the slice's learner (and exchange) on the same stream
+__global__ void __launch_bounds__(256) k_group_snap(const GroupRollout* __restrict__ tab, int par) {
+  const GroupRollout& T = tab[blockIdx.y];
+  const int p0 = par < 0 ? 0 : par, p1 = par < 0 ? 1 : par;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < 6 * nn::NP; i += gridDim.x * blockDim.x) {
+    const float v = T.A.w[i];
+    for (int p = p0; p <= p1; ++p) T.snap[(size_t)p * 6 * nn::NP + i] = v;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < 2)
+    for (int p = p0; p <= p1; ++p) T.snap_eps[2 * p + threadIdx.x] = T.A.st->epsilon[threadIdx.x];
 }
 
 // ---------------------------------------------------------------------------
@@ -520,7 +543,6 @@ int engine_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, bool own_streams, n
   NFSP_REQUIRE(cfg->slices >= 1 && cfg->n_lanes % cfg->slices == 0,
                "slices must be >= 1 and divide n_lanes");
   NFSP_REQUIRE(cfg->slice_lag == 1 || cfg->slice_lag == 2, "slice_lag must be 1 or 2");
-  NFSP_REQUIRE(cfg->slice_lag == 1 || own_streams, "engine groups run with slice_lag 1");
   NFSP_REQUIRE(cfg->fit_batch == CHAIN_MB, "the SGD chains are built for fit_batch == 32");
   NFSP_REQUIRE(cfg->batch >= CHAIN_MB && cfg->batch <= MAX_BATCH && cfg->batch % CHAIN_MB == 0,
                "batch must be 32, 64, 96 or 128");
@@ -574,7 +596,7 @@ int engine_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, bool own_streams, n
   // (cfg.slice_lag 2: two sets, slice parity; the reservoir lists are shared -- only the
   // ctx stream's prep kernels use them, in slice order)
   e->slice_lag = cfg->slice_lag;
-  for (int k = 0; k < (e->slice_lag == 2 ? 2 : 1); ++k) {
+  for (int k = 0; k < (e->slice_lag == 2 && own_streams ? 2 : 1); ++k) {
     LearnBufs& L = e->LBs[k];
     L.umax = 4 * N / cfg->inserts_per_update + 2;
     const int64_t ub = 2 * L.umax * cfg->batch, ueb = ub * cfg->epochs;
@@ -599,6 +621,7 @@ int engine_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, bool own_streams, n
   e->LB = e->LBs[0];
   if (e->slice_lag == 2) {
     EALLOC(e->snap, sizeof(float) * 2 * 6 * nn::NP);
+    if (!own_streams) EALLOC(e->snap_eps_dev, sizeof(double) * 4);   // a group replica
     for (auto& pe : e->snap_ev)
       for (hipEvent_t& ev : pe) {
         const hipError_t er = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
@@ -710,6 +733,8 @@ int group_rollout_table(nfsp_engine* const* eng, int R, void** d_tab) {
     h[r].A = rollout_args(eng[r]);
     h[r].M = eng[r]->M;
     h[r].nblk = eng[r]->nblk;
+    h[r].snap = eng[r]->snap;
+    h[r].snap_eps = eng[r]->snap_eps_dev;
   }
   NFSP_HIP(hipMalloc(d_tab, sizeof(GroupRollout) * R));
   NFSP_HIP(hipMemcpy(*d_tab, h.data(), sizeof(GroupRollout) * R, hipMemcpyHostToDevice));
@@ -718,7 +743,7 @@ int group_rollout_table(nfsp_engine* const* eng, int R, void** d_tab) {
 
 // every replica's rollout in one launch per kernel (blockIdx.y = replica); the marks are
 // kept on replica 0
-int group_rollout_launch(nfsp_engine* const* eng, int R, const void* d_tab) {
+int group_rollout_launch(nfsp_engine* const* eng, int R, const void* d_tab, int par) {
   nfsp_engine* e0 = eng[0];
   for (int r = 0; r < R; ++r)
     NFSP_REQUIRE(!eng[r]->pending_update && eng[r]->rollouts == e0->rollouts,
@@ -728,7 +753,7 @@ int group_rollout_launch(nfsp_engine* const* eng, int R, const void* d_tab) {
   {
     KTimer kt(e0, KT_ROLLOUT);
     const RolloutArgs A0 = rollout_args(e0);   // slice and hand index, the same for every replica
-    k_rollout_g<<<dim3(e0->nblk, R), 256, 0, s>>>(tab, A0.g_lo, A0.g_hi, A0.lane0);
+    k_rollout_g<<<dim3(e0->nblk, R), 256, 0, s>>>(tab, A0.g_lo, A0.g_hi, A0.lane0, par);
   }
   NFSP_LAUNCHED("k_rollout_g");
   {
@@ -748,6 +773,15 @@ int group_rollout_launch(nfsp_engine* const* eng, int R, const void* d_tab) {
     eng[r]->rollouts++;
     eng[r]->pending_update = true;
   }
+  return NFSP_OK;
+}
+
+int group_snap_launch(nfsp_engine* const* eng, int R, const void* d_tab, int par) {
+  for (int r = 0; r < R; ++r)
+    NFSP_REQUIRE(eng[r]->snap && eng[r]->snap_eps_dev, "group replica without snapshots (slice_lag 1)");
+  k_group_snap<<<dim3(nfsp_blocks(6 * nn::NP, 256), R), 256, 0, eng[0]->ctx->stream>>>(
+      static_cast<const GroupRollout*>(d_tab), par);
+  NFSP_LAUNCHED("k_group_snap");
   return NFSP_OK;
 }
 }  // namespace eng

@@ -152,7 +152,8 @@ enum {
   KT_ROLLOUT = 0, KT_SCAN = 1, KT_COMMIT = 2, KT_LEARNER = 3,   // LEARNER = whole update call
   KT_PREP = 4, KT_TARGETS = 5, KT_CHAIN_BR = 6, KT_CHAIN_AR = 7,
   KT_BR_STREAM0 = 8, KT_BR_STREAM1 = 9,   // span of agent a's BR stream (first targets .. last chain)
-  KT_N = 10
+  KT_XCHG = 10,                           // the cross-shard AR exchange (delta, all-reduce, apply)
+  KT_N = 11
 };
 
 // Stage packed weights (W1[30][64] | b1 | W2 | b2) into the padded LDS layout of fwd_lds.
@@ -267,6 +268,16 @@ struct nfsp_engine {
   float* snap = nullptr;
   double snap_eps[2][2] = {};
   hipEvent_t snap_ev[2][3] = {};     // [parity][AR stream, BR stream 0, BR stream 1]
+  double* snap_eps_dev = nullptr;    // a group replica's (slice_lag 2): [parity][agent], on device
+  // the cross-shard AR exchange (nfsp_engine_set_exchange; exchange.hip)
+  int xchg_every = 0;                // learner calls between exchanges (0: off)
+  int64_t xchg_calls = 0, xchg_done = 0;
+  float xchg_scale = 1.f;
+  float* xchg_w0 = nullptr;          // [2][NP] the AR nets after the last exchange
+  float* xchg_buf = nullptr;         // [2][NP] D, then the sum over shards
+  void* xchg_comm = nullptr;         // RCCL communicator, or
+  nfsp_exchange_fn xchg_fn = nullptr;  // the host transport
+  void* xchg_user = nullptr;
   // host mirror of the schedules (agent/agent.py:245-253, 266-273): plan_update computes them
   // in the reference's double arithmetic; k_finalize publishes them to EngineDev for the stats
   struct Sched {
@@ -298,7 +309,12 @@ int step_pipelined(nfsp_engine* e);
 // engine groups: the replicas' rollout arguments as a device table (static), and every
 // replica's rollout through it in one launch per kernel
 int group_rollout_table(nfsp_engine* const* eng, int R, void** d_tab);
-int group_rollout_launch(nfsp_engine* const* eng, int R, const void* d_tab);
+// par: the snapshot parity the slice acts with (slice_lag 2), -1: the replicas' own nets
+int group_rollout_launch(nfsp_engine* const* eng, int R, const void* d_tab, int par);
+// slice_lag 2: every replica's nets and epsilon -> snapshot par (-1: both parities)
+int group_snap_launch(nfsp_engine* const* eng, int R, const void* d_tab, int par);
+// the cross-shard exchange of the AR nets, enqueued on `s` (the AR chain stream)
+int exchange_enqueue(nfsp_engine* e, hipStream_t s);
 
 // RAII bracket: records start/stop events around launches on `stream` when timing is on
 struct KTimer {

@@ -410,17 +410,22 @@ __global__ void k_finalize(FinalArgs F0, const FinalArgs* __restrict__ tab, int 
   }
 }
 
-// engine groups: the AR nets of all replicas <- W0 + sum_r (W_r - W0) / R, and W0 <- that
-// (shards.AvgPolicyAllReduce's exchange, on device, in replica order)
-__global__ void __launch_bounds__(256) k_group_avg_ar(float* const* __restrict__ war /*[R][2]*/,
-                                                      float* __restrict__ w0 /*[2][NP]*/, int R,
-                                                      int broadcast) {
+// engine groups: the exchanged nets of all replicas <- W0 + (sum_r (W_r - W0)) * scale, and W0 <-
+// that (nfsp_engine_set_exchange's arithmetic over shards, on device, in replica order).
+// wtab [3 nets: AR, BR, target][R][2 agents]; nets / bcast: masks over the 3 (bcast: the first
+// exchange of a net copies replica 0's everywhere)
+__global__ void __launch_bounds__(256) k_group_xchg(float* const* __restrict__ wtab, float* __restrict__ w0 /*[3][2][NP]*/,
+                                                    int R, unsigned nets, unsigned bcast, float scale) {
 #pragma clang fp contract(off)
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= 2 * nn::NP) return;
-  const int a = i / nn::NP, q = i - a * nn::NP;
+  if (i >= 3 * 2 * nn::NP) return;
+  const int n = i / (2 * nn::NP), k = i - n * 2 * nn::NP;
+  const int a = k / nn::NP, q = k - a * nn::NP;
+  const bool b = (bcast >> n) & 1u;
+  if (!b && !((nets >> n) & 1u)) return;
+  float* const* war = wtab + (size_t)n * R * 2;
   float nw;
-  if (broadcast) {                      // the first exchange: replica 0's nets everywhere
+  if (b) {
     nw = war[a][q];
   } else {
     const float base = w0[i];
@@ -429,7 +434,7 @@ __global__ void __launch_bounds__(256) k_group_avg_ar(float* const* __restrict__
     // (one at a time, R = 256 took 0.2 ms of latency per step)
 #pragma unroll 16
     for (int r = 0; r < R; ++r) s = s + (war[2 * r + a][q] - base);
-    nw = base + s * (1.0f / (float)R);
+    nw = base + s * scale;
   }
   w0[i] = nw;
   for (int r = 0; r < R; ++r) war[2 * r + a][q] = nw;
@@ -673,7 +678,9 @@ static int update_impl(nfsp_engine* e, bool pipelined, int par, bool snap_after)
   int rc = plan_update(e, h, L);
   if (rc != NFSP_OK) return rc;
   e->pending_update = false;
-  if (pipelined)                       // the rollout two slices on acts with this epsilon
+  // the cross-shard exchange after this call's AR chain (nfsp_engine_set_exchange)
+  const bool xchg = e->xchg_every > 0 && (++e->xchg_calls) % e->xchg_every == 0;
+  if (pipelined && snap_after)         // the rollout two slices on acts with this epsilon
     for (int a = 0; a < 2; ++a) e->snap_eps[par][a] = e->hs.epsilon[a];
   // ---- parallel prep on the ctx stream, in the order the chains need it: the BR rows
   // first (agent 0's BR segments are the learner's critical path), the BR streams fork;
@@ -701,15 +708,19 @@ static int update_impl(nfsp_engine* e, bool pipelined, int par, bool snap_after)
     C.E = cfg.epochs;
     for (int a = 0; a < 2; ++a) {
       C.job[a] = ar_job(e, L, a);
-      if (snap_after) C.job[a].snap_to = snap + (a * 3 + 0) * nn::NP;   // written by the chain
+      if (snap_after && !xchg) C.job[a].snap_to = snap + (a * 3 + 0) * nn::NP;   // written by the chain
     }
     KTimer kc(e, KT_CHAIN_AR, e->s_ar);
     if ((rc = launch_chain_ar(C, 2, e->log_loss, e->s_ar)) != NFSP_OK) return rc;
-  } else if (snap_after) {
+  }
+  if (xchg) {
+    KTimer kx(e, KT_XCHG, e->s_ar);
+    if ((rc = exchange_enqueue(e, e->s_ar)) != NFSP_OK) return rc;
+  }
+  if (snap_after && (xchg || L.maxU == 0))   // the AR nets as they are now (exchanged)
     for (int a = 0; a < 2; ++a)
       NFSP_HIP(hipMemcpyAsync(snap + (a * 3 + 0) * nn::NP, e->w + (a * 3 + 0) * nn::NP,
                               sizeof(float) * nn::NP, hipMemcpyDeviceToDevice, e->s_ar));
-  }
   if (snap_after) NFSP_HIP(hipEventRecord(e->snap_ev[par][0], e->s_ar));
   // diagnostic (NFSP_LEARNER_SERIAL=1): BR work waits for the AR chains, to time them alone
   static const bool serial_ar = getenv("NFSP_LEARNER_SERIAL") && atoi(getenv("NFSP_LEARNER_SERIAL"));
@@ -834,9 +845,13 @@ struct nfsp_group {
   EngineDev** d_stp = nullptr;   // [R] -> each replica's state
   EngineDev* d_st = nullptr;     // [R]
   EngineDev* h_st = nullptr;     // [R] pinned
-  float** d_war = nullptr;       // [R][2] AR weight pointers (k_group_avg_ar)
-  float* w0 = nullptr;           // [2][NP] the AR nets after the last exchange
-  bool w0_valid = false;
+  float** d_war = nullptr;       // [3 nets][R][2] weight pointers (k_group_xchg)
+  float* w0 = nullptr;           // [3][2][NP] the exchanged nets after the last exchange
+  unsigned w0_valid = 0;         // nets (NFSP_XCHG_*) broadcast from replica 0 already
+  unsigned xchg_nets = 0;        // nfsp_group_set_exchange
+  int xchg_every = 0;
+  float xchg_scale = 1.f;
+  int64_t calls = 0;             // learner calls (slices) so far
   int64_t rounds = 0;            // BR rounds of the last learner call (stats)
   int chain_lds = 0;             // LDS per chain workgroup: 4R chains on the device's CUs
 };
@@ -873,6 +888,7 @@ extern "C" int nfsp_group_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, int 
   NFSP_REQUIRE(ctx && cfg && out, "null argument");
   NFSP_REQUIRE(replicas >= 1 && replicas <= NFSP_GROUP_MAX_REPLICAS, "replicas must be in [1, 256]");
   NFSP_REQUIRE((flags & ~NFSP_GROUP_AVG_AR) == 0, "unknown group flags");
+  NFSP_REQUIRE(cfg->slices >= 1, "slices must be >= 1");
   *out = nullptr;
   // up to 4R chain workgroups run at once (2R AR + a BR round's 2R): past one per CU they
   // share CUs, each with an equal share of the LDS
@@ -883,6 +899,11 @@ extern "C" int nfsp_group_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, int 
   g->ctx = ctx;
   g->R = replicas;
   g->flags = flags;
+  if (flags & NFSP_GROUP_AVG_AR) {     // the per-step AR exchange
+    g->xchg_nets = NFSP_XCHG_AR;
+    g->xchg_every = cfg->slices;
+    g->xchg_scale = 1.0f / (float)replicas;
+  }
   g->chain_lds = chain_lds_shared((4 * replicas + cus - 1) / (cus > 0 ? cus : 1));
   for (int r = 0; r < replicas; ++r) {
     nfsp_engine_cfg c = *cfg;
@@ -907,14 +928,15 @@ extern "C" int nfsp_group_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, int 
     nfsp_group_destroy(g);
     return rc;
   }
-  std::vector<float*> war(2 * replicas);
+  std::vector<float*> war(3 * 2 * replicas);
   std::vector<EngineDev*> stp(replicas);
   for (int r = 0; r < replicas; ++r) {
-    for (int a = 0; a < 2; ++a) war[2 * r + a] = g->eng[r]->w + (a * 3 + 0) * nn::NP;
+    for (int n = 0; n < 3; ++n)
+      for (int a = 0; a < 2; ++a) war[((size_t)n * replicas + r) * 2 + a] = g->eng[r]->w + (a * 3 + n) * nn::NP;
     stp[r] = g->eng[r]->st;
   }
   hipError_t r = hipMalloc((void**)&g->d_war, sizeof(float*) * war.size());
-  if (r == hipSuccess) r = hipMalloc((void**)&g->w0, sizeof(float) * 2 * nn::NP);
+  if (r == hipSuccess) r = hipMalloc((void**)&g->w0, sizeof(float) * 3 * 2 * nn::NP);
   if (r == hipSuccess) r = hipMemcpy(g->d_war, war.data(), sizeof(float*) * war.size(), hipMemcpyHostToDevice);
   if (r == hipSuccess) r = hipMalloc((void**)&g->d_stp, sizeof(EngineDev*) * replicas);
   if (r == hipSuccess) r = hipMalloc((void**)&g->d_st, sizeof(EngineDev) * replicas);
@@ -936,10 +958,26 @@ extern "C" int nfsp_group_engine(nfsp_group* g, int r, nfsp_engine** out) {
 
 extern "C" int nfsp_group_average_ar(nfsp_group* g) {
   NFSP_REQUIRE(g, "null argument");
-  k_group_avg_ar<<<nfsp_blocks(2 * nn::NP, 256), 256, 0, g->ctx->stream>>>(g->d_war, g->w0, g->R,
-                                                                           g->w0_valid ? 0 : 1);
-  NFSP_LAUNCHED("k_group_avg_ar");
-  g->w0_valid = true;
+  const unsigned nets = g->xchg_nets ? g->xchg_nets : NFSP_XCHG_AR;
+  // nets not broadcast yet take replica 0's (a BR net with its target net)
+  unsigned bc = nets & ~g->w0_valid;
+  if (bc & NFSP_XCHG_BR) bc |= 4u;
+  const float scale = g->xchg_nets ? g->xchg_scale : 1.0f / (float)g->R;
+  k_group_xchg<<<nfsp_blocks(3 * 2 * nn::NP, 256), 256, 0, g->ctx->stream>>>(g->d_war, g->w0, g->R, nets,
+                                                                            bc, scale);
+  NFSP_LAUNCHED("k_group_xchg");
+  g->w0_valid |= nets;
+  return NFSP_OK;
+}
+
+extern "C" int nfsp_group_set_exchange(nfsp_group* g, unsigned nets, int every, float scale) {
+  NFSP_REQUIRE(g, "null argument");
+  NFSP_REQUIRE((nets & ~(NFSP_XCHG_AR | NFSP_XCHG_BR)) == 0, "nets: NFSP_XCHG_AR | NFSP_XCHG_BR");
+  NFSP_REQUIRE(every >= 0 && (every == 0 || nets), "every >= 0 (and nets when on)");
+  g->xchg_nets = every ? nets : 0;
+  g->xchg_every = every;
+  g->xchg_scale = scale;
+  g->calls = 0;
   return NFSP_OK;
 }
 
@@ -1132,6 +1170,12 @@ extern "C" int nfsp_engine_snapshot(nfsp_engine* e, int parity, float** dev_w, d
   NFSP_REQUIRE(e && dev_w && eps && (parity == 0 || parity == 1), "bad argument");
   NFSP_REQUIRE(e->snap, "the engine has no snapshots (cfg.slice_lag 1)");
   *dev_w = e->snap + (size_t)parity * 6 * nn::NP;
+  if (e->snap_eps_dev) {               // a group replica: its snapshots' epsilons are on device
+    NFSP_HIP(hipMemcpyAsync(eps, e->snap_eps_dev + 2 * parity, 2 * sizeof(double), hipMemcpyDeviceToHost,
+                            e->ctx->stream));
+    NFSP_HIP(hipStreamSynchronize(e->ctx->stream));
+    return NFSP_OK;
+  }
   eps[0] = e->snap_eps[parity][0];
   eps[1] = e->snap_eps[parity][1];
   return NFSP_OK;
@@ -1163,16 +1207,27 @@ extern "C" int nfsp_group_get_timings(nfsp_group* g, double* ms, int64_t* launch
   return NFSP_OK;
 }
 
+// Every slice: rollout, then its learner, then (when due) the exchange.  With slice_lag 2 the
+// slices run one after another, but slice j acts with snapshot j & 1: the nets and epsilon as
+// slice j - 2's learner (and exchange) left them, the step's start for j < 2 -- a pipelined
+// engine's arithmetic (step_pipelined).
 extern "C" int nfsp_group_step(nfsp_group* g) {
   NFSP_REQUIRE(g, "null argument");
   int rc;
-  if ((g->flags & NFSP_GROUP_AVG_AR) && !g->w0_valid)      // common AR nets before the first step
+  if (g->xchg_nets & ~g->w0_valid)      // common nets before the first exchange
     if ((rc = nfsp_group_average_ar(g)) != NFSP_OK) return rc;
-  for (int k = 0; k < g->eng[0]->slices; ++k) {    // every slice: rollout, then its learner
-    if ((rc = nfsp::eng::group_rollout_launch(g->eng.data(), g->R, g->d_roll)) != NFSP_OK) return rc;
+  const int K = g->eng[0]->slices;
+  const bool lag2 = g->eng[0]->slice_lag == 2 && K > 1;
+  if (lag2 && (rc = nfsp::eng::group_snap_launch(g->eng.data(), g->R, g->d_roll, -1)) != NFSP_OK) return rc;
+  for (int j = 0; j < K; ++j) {
+    if ((rc = nfsp::eng::group_rollout_launch(g->eng.data(), g->R, g->d_roll, lag2 ? (j & 1) : -1)) != NFSP_OK)
+      return rc;
     if ((rc = group_update(g)) != NFSP_OK) return rc;
+    if (g->xchg_every > 0 && (++g->calls) % g->xchg_every == 0 && (rc = nfsp_group_average_ar(g)) != NFSP_OK)
+      return rc;
+    if (lag2 && j + 2 < K && (rc = nfsp::eng::group_snap_launch(g->eng.data(), g->R, g->d_roll, j & 1)) != NFSP_OK)
+      return rc;
   }
-  if (g->flags & NFSP_GROUP_AVG_AR) return nfsp_group_average_ar(g);
   return NFSP_OK;
 }
 

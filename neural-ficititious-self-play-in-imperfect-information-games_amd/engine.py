@@ -123,7 +123,7 @@ class SelfPlayEngine:
         return s.to_dict()
 
     KERNELS = ("k_rollout", "k_scan", "k_commit", "learner", "learner_prep", "k_br_targets",
-               "k_chain3_br", "k_chain3_ar", "br_stream_a0", "br_stream_a1")
+               "k_chain3_br", "k_chain3_ar", "br_stream_a0", "br_stream_a1", "ar_exchange")
 
     def set_timing(self, on=True):
         native.check(self.L.nfsp_engine_set_timing(self.h, int(bool(on))), "set_timing")
@@ -202,6 +202,20 @@ class SelfPlayEngine:
         w = _wrap_device(p.value, 6 * NP, torch.float32, self.dev, self).cpu().numpy().copy()
         return w, (eps[0], eps[1])
 
+    def set_exchange(self, every: int, scale: float, comm=None, fn=None):
+        """The cross-shard exchange of the AR nets (nfsp_engine_set_exchange): after every
+        ``every``-th learner call (slice), W_AR = W0 + (sum over shards of W_AR - W0) * scale on
+        the AR chain stream, by the RCCL communicator ``comm`` or the host callback ``fn``
+        (a ``native.EXCHANGE_FN``; kept alive here).  W0 = the AR nets now.  every 0: off."""
+        self._xchg_fn = fn
+        native.check(self.L.nfsp_engine_set_exchange(self.h, int(every), float(scale), comm, fn, None),
+                     "nfsp_engine_set_exchange")
+
+    def exchanges(self) -> int:
+        n = native.I64()
+        native.check(self.L.nfsp_engine_exchanges(self.h, C.byref(n)), "nfsp_engine_exchanges")
+        return n.value
+
     def set_update_limit(self, max_updates: int):
         """Test hook (nfsp_engine_set_update_limit): the chains run only a prefix of each
         learner call's updates."""
@@ -248,7 +262,9 @@ class EngineGroup:
     initial nets from ``init_seed + r`` -- replica r is bit-identical to
     ``SelfPlayEngine(seed=seed + r, init_seed=init_seed + r)``), their SGD chains in shared
     launches.  ``avg_ar``: the AR nets are averaged over the replicas after every step (C4's
-    exchange on device, shards.AvgPolicyAllReduce)."""
+    exchange on device, shards.AvgPolicyAllReduce); ``set_exchange`` for other cadences (e.g.
+    after every slice, shards.AvgPolicyExchange's).  ``slice_lag=2``: every replica's slice j
+    acts with the nets slice j - 2 left (a pipelined engine's arithmetic, run serially)."""
 
     def __init__(self, replicas: int, ctx: native.Context | None = None, init_seed: int = 0,
                  game: int = native.GAME_LEDUC, avg_ar: bool = False, **cfg):
@@ -274,6 +290,15 @@ class EngineGroup:
 
     def average_ar(self):
         native.check(self.L.nfsp_group_average_ar(self.h), "nfsp_group_average_ar")
+
+    def set_exchange(self, nets: int = native.XCHG_AR, every: int = 1, scale: float | None = None):
+        """nfsp_group_set_exchange: after every ``every``-th slice, the ``nets``
+        (native.XCHG_AR | XCHG_BR) of all replicas <- W0 + (sum_r W_r - W0) * scale (default
+        1 / R, the mean); every 0: off.  The next exchange of a net not exchanged before copies
+        replica 0's instead."""
+        scale = 1.0 / self.R if scale is None else float(scale)
+        native.check(self.L.nfsp_group_set_exchange(self.h, int(nets), int(every), scale),
+                     "nfsp_group_set_exchange")
 
     def rounds(self) -> int:
         n = native.I64()

@@ -120,8 +120,17 @@ SIGNATURES = {
     "nfsp_group_set_timing": (I32, [P, I32]),
     "nfsp_group_get_timings": (I32, [P, C.POINTER(F64), C.POINTER(I64)]),
     "nfsp_group_rounds": (I32, [P, C.POINTER(I64)]),
+    "nfsp_group_set_exchange": (I32, [P, U32, I32, F32]),
+    "nfsp_engine_set_exchange": (I32, [P, I32, F32, P, P, P]),
+    "nfsp_engine_exchanges": (I32, [P, C.POINTER(I64)]),
+    "nfsp_rccl_unique_id": (I32, [P]),
+    "nfsp_rccl_comm_create": (I32, [P, I32, I32, I32, C.POINTER(P)]),
+    "nfsp_rccl_comm_destroy": (I32, [P]),
 }
+# int (*nfsp_exchange_fn)(void* user, float* dev_sum, int64_t n)
+EXCHANGE_FN = C.CFUNCTYPE(C.c_int, P, P, I64)
 GROUP_AVG_AR = 1
+XCHG_AR, XCHG_BR = 1, 2
 DEAL_PHILOX, DEAL_PY3_MT, DEAL_PY2_MT = 0, 1, 2
 GROUP_MAX_REPLICAS = 256
 

@@ -1,8 +1,19 @@
 """Multi-GPU self-play shards (BASELINE.json configs[3] = C4).
 
 One process per GPU, each with its own ``SelfPlayEngine`` (its own hands, memories and
-learner; seeds 1234 + rank).  Hands never cross GPUs.  The one exchange is the optional
-all-reduce of the average-policy (AR) gradients of both agents over RCCL:
+learner; seeds 1234 + rank).  Hands never cross GPUs.  The one exchange is the all-reduce of
+the average-policy (AR) gradient steps of both agents.
+
+``AvgPolicyExchange`` (what bench.py runs at N > 1) does it inside the engine, after every
+lane slice's learner (nfsp_engine_set_exchange): the reference learns inside its hand loop
+(main.py:27-67, an update every 128 RL inserts, agent/agent.py:153-154), so the shards' AR
+copies are merged every 65,536 hands per rank rather than once per 1M-hand step.  On RCCL the
+collective is enqueued by libnfsp itself on the AR chain stream (ncclAllReduce on a
+communicator of its own), behind the slice's AR chain and before the snapshot the rollout two
+slices on acts with -- no host round trip.  Over gloo (CPU rehearsals, co-resident tests) a
+host callback sums the deltas through the process group instead, with the same arithmetic.
+
+``AvgPolicyAllReduce`` is the per-step exchange of round 3 from the host, between steps:
 
 * ``AvgPolicyAllReduce(tensors, dist)`` first broadcasts rank 0's AR nets, so every shard's
   AR nets start equal;
@@ -24,6 +35,9 @@ the collective (``torch.cuda.synchronize`` on a GPU).
 """
 from __future__ import annotations
 
+import ctypes as C
+import sys
+import traceback
 from typing import Callable, Sequence
 
 import torch
@@ -77,3 +91,89 @@ class AvgPolicyAllReduce:
         self._scatter(self.base)
         self.sync()                                  # the next rollout reads the new nets
         self.calls += 1
+
+
+class AvgPolicyExchange:
+    """The AR exchange inside the engine, every ``every`` learner calls (slices): W0 + gain x
+    the mean over ranks of (W_r - W0) after each slice's AR chain (include/nfsp.h
+    nfsp_engine_set_exchange, scale = gain / world).  gain 1 is plain model averaging
+    (data-parallel SGD of one net over every shard's minibatches, exchanged per slice); gain g
+    is a server step g x the mean of the shards' steps.  ``transport``: "rccl"
+    (libnfsp's own communicator, the collective on the AR chain stream), "host" (the process
+    group's all-reduce from a host callback: gloo), or "auto" (rccl under the nccl backend,
+    host otherwise)."""
+
+    def __init__(self, engine, dist, every: int = 1, transport: str = "auto", gain: float = 1.0,
+                 src: int = 0):
+        from . import native
+        from .engine import NET_AR, _wrap_device
+        self.engine, self.dist, self.every, self.gain = engine, dist, int(every), float(gain)
+        self.world, self.rank = dist.get_world_size(), dist.get_rank()
+        backend = dist.get_backend()
+        self.transport = ("rccl" if backend == "nccl" else "host") if transport == "auto" else transport
+        self._wrap, self._dev = _wrap_device, engine.dev
+        # the common start: rank 0's AR nets everywhere (one broadcast)
+        torch.cuda.synchronize()
+        views = [engine.weights_tensor(a, NET_AR) for a in (0, 1)]
+        flat = torch.cat([v.reshape(-1) for v in views])
+        if backend == "gloo":
+            x = flat.cpu()
+            dist.broadcast(x, src=src)
+            flat.copy_(x)
+        else:
+            dist.broadcast(flat, src=src)
+        off = 0
+        for v in views:
+            v.copy_(flat[off:off + v.numel()])
+            off += v.numel()
+        torch.cuda.synchronize()
+        self.bytes_per_call = 4 * flat.numel()
+        self.comm = None
+        self._fn = None
+        L = engine.L
+        if self.transport == "rccl":
+            uid = (C.c_uint8 * 128)()
+            if self.rank == src:
+                native.check(L.nfsp_rccl_unique_id(uid), "nfsp_rccl_unique_id")
+            dev = "cuda" if backend == "nccl" else "cpu"
+            t = torch.tensor(list(uid), dtype=torch.uint8, device=dev)
+            dist.broadcast(t, src=src)
+            uid = (C.c_uint8 * 128)(*t.cpu().tolist())
+            comm = native.P()
+            native.check(L.nfsp_rccl_comm_create(uid, self.world, self.rank, torch.cuda.current_device(),
+                                                  C.byref(comm)), "nfsp_rccl_comm_create")
+            self.comm = comm
+            engine.set_exchange(self.every, self.gain / self.world, comm=comm)
+        elif self.transport == "host":
+            self._fn = native.EXCHANGE_FN(self._host_sum)
+            engine.set_exchange(self.every, self.gain / self.world, fn=self._fn)
+        else:
+            raise ValueError(f"unknown transport {transport!r}")
+
+    def _host_sum(self, _user, ptr, n):
+        """nfsp_exchange_fn: the engine synchronised its AR stream; leave the sum over ranks
+        of the [2][NP] deltas at ptr (device), complete on return."""
+        try:
+            t = self._wrap(ptr, n, torch.float32, self._dev)
+            x = t.cpu()
+            if self.dist.get_backend() == "gloo":
+                self.dist.all_reduce(x)
+                t.copy_(x)
+            else:
+                self.dist.all_reduce(t)
+            torch.cuda.synchronize()
+            return 0
+        except BaseException:           # never unwind through the C caller
+            traceback.print_exc(file=sys.stderr)
+            return 1
+
+    @property
+    def calls(self) -> int:
+        return self.engine.exchanges()
+
+    def close(self):
+        if self.engine.h is not None:
+            self.engine.set_exchange(0, 1.0)
+        if self.comm is not None:
+            self.engine.L.nfsp_rccl_comm_destroy(self.comm)
+            self.comm = None

@@ -66,6 +66,22 @@ def test_gpus_flag_launches_the_ranks():
     # rank 1 sleeps 1.5x as long: the job time is the slow rank's
     assert out["ms_per_step"] >= 30.0
     assert abs(out["value"] - 2 * 3 * 65_536 / (out["ms_per_step"] * 3e-3)) < 1e-6 * out["value"]
+    # N > 1 explains itself: every rank's own step time, device / PCI bus id, exchange cost
+    rk = out["ranks"]
+    assert rk["world_size"] == 2 and [r["rank"] for r in rk["ranks"]] == [0, 1]
+    ms = [r["ms_per_step"] for r in rk["ranks"]]
+    assert 20.0 <= ms[0] < ms[1] and ms[1] >= 30.0
+    assert rk["ms_per_step_min"] == ms[0] and rk["ms_per_step_max"] == ms[1]
+    assert out["ms_per_step"] >= ms[1]            # the job waits for the slowest rank
+    for r in rk["ranks"]:
+        for k in ("device", "pci_bus_id", "host", "exchange_ms_per_call", "exchanges"):
+            assert k in r, (k, r)
+
+
+def test_one_rank_line_has_no_rank_report():
+    rc, lines, err = _bench(["--steps", "2", "--warmup", "0", "--stub-step-ms", "5"])
+    assert rc == 0, err
+    assert len(lines) == 1 and lines[0]["n_gpus"] == 1 and "ranks" not in lines[0]
 
 
 def test_world_size_mismatch_refused():

@@ -1,0 +1,87 @@
+"""bench.py's roofline arithmetic on the committed measurements (no GPU): every framing of every
+kernel stays at or below its peak, and the rollout's HBM framing counts the lanes ONE launch
+plays (one slice: n_lanes / slices), not the whole step's.  Round 3's line divided the step's
+1M lanes' bytes by one 65,536-lane launch's duration and reported frac 2.1.
+Inputs: the event-timed pass of profiles/r03_bench_default.json (kernel_ms = ms per launch,
+kernel_ms_per_step = ms per step, per_step = the pass's updates and inserts)."""
+import json
+import math
+import os
+
+import pytest
+
+from conftest import REPO
+
+PROFILES = [("r03_bench_default.json", "c3"), ("r03_c2_bench.json", "c2"), ("r03_c5_bench.json", "c5"),
+            ("r03_c5_tb_bench.json", "c5_tb")]
+
+
+def _inputs(d):
+    steps = d["steps"]
+    k_ms, k_step = d["kernel_ms"], d["kernel_ms_per_step"]
+    k_ms = dict(k_ms, ar_exchange=k_ms.get("ar_exchange", 0.0))
+    k_step = dict(k_step, ar_exchange=k_step.get("ar_exchange", 0.0))
+    launches = {k: (round(k_step[k] * steps / k_ms[k]) if k_ms[k] > 0 else 0) for k in k_ms}
+    ps = d["per_step"]
+    br, ar = ps["br_updates"] * steps, ps["ar_updates"] * steps
+    ar_max = ps.get("ar_updates_max_chain", ps["ar_updates"] / 2) * steps
+    hands_per_s = d["value"] / d["n_gpus"]
+    return k_ms, launches, k_step, br, ar, ar_max, ps["rl_inserts_per_hand"], ps["sl_inserts_per_hand"], hands_per_s
+
+
+def _frac_values(obj):
+    if isinstance(obj, dict):
+        for k, v in obj.items():
+            if k.startswith("frac") and isinstance(v, (int, float)):
+                yield k, v
+            else:
+                yield from _frac_values(v)
+
+
+@pytest.mark.parametrize("name,config", PROFILES)
+def test_every_frac_at_most_one(name, config):
+    import bench
+    with open(os.path.join(REPO, "profiles", name)) as f:
+        d = json.load(f)
+    cfg = dict(bench.CONFIGS[config], slices=d.get("slices", 1), slice_lag=d.get("slice_lag", 1))
+    roof, other, whole, streams = bench.rooflines(config, cfg, *_inputs(d))
+    fr = list(_frac_values({"roofline": roof, "other": other, "whole": whole}))
+    assert len(fr) >= 8
+    for k, v in fr:
+        assert 0.0 <= v <= 1.0, (name, k, v)
+    # the rollout: the reference-layout bytes of the hands one launch plays
+    r = other["k_rollout_hbm"]
+    lanes = cfg["n_lanes"] // cfg["slices"]
+    assert r["lanes_per_launch"] == lanes
+    exp = r["bytes_per_hand"] * lanes / (d["kernel_ms"]["k_rollout"] * 1e-3) / 1e9 / bench.PEAK_HBM_GBS
+    assert math.isclose(r["frac"], exp, rel_tol=1e-12)
+    # the critical stream's chain is the roofline kernel
+    assert roof["critical_stream"] == max(streams, key=streams.get)
+    assert other["k_chain3_ar_mfma"]["peak"] == bench.PEAK_BF16_TFLOPS
+
+
+def test_c3_rollout_frac_reproduces_from_the_kernel_stats():
+    """C3's rollout: ~1.44 KB of reference-layout tuples per hand x 65,536 lanes per launch over
+    the launch's 0.09 ms = ~1.05 TB/s, frac ~0.13 -- the same figure from the rocprofv3 average
+    of the same tree's launches (profiles/r03_c3_kernel_stats.csv)."""
+    import bench
+    with open(os.path.join(REPO, "profiles", "r03_bench_default.json")) as f:
+        d = json.load(f)
+    cfg = dict(bench.CONFIGS["c3"])
+    _, other, _, _ = bench.rooflines("c3", cfg, *_inputs(d))
+    r = other["k_rollout_hbm"]
+    assert 0.11 <= r["frac"] <= 0.15, r
+    # the rocprof average duration of k_rollout in the committed kernel stats
+    import csv
+    with open(os.path.join(REPO, "profiles", "r03_c3_kernel_stats.csv")) as f:
+        rows = [row for row in csv.DictReader(f) if "::k_rollout(" in row["Name"]]
+    assert rows
+    avg_ms = float(rows[0]["AverageNs"]) * 1e-6
+    frac_rocprof = r["bytes_per_hand"] * 65_536 / (avg_ms * 1e-3) / 1e9 / bench.PEAK_HBM_GBS
+    assert abs(frac_rocprof - r["frac"]) <= 0.02, (frac_rocprof, r["frac"])
+
+
+def test_cpu_share_is_bounded_by_the_machine():
+    import bench
+    n = bench.cpu_share()
+    assert 1 <= n <= (os.cpu_count() or 1)

@@ -15,8 +15,8 @@ update trigger agent/agent.py:153-154).
   lanes, 16 slices, M_RL 200k, M_SL 2M) against the CPU seed band of the reference's
   main.train restated in C++ with the same memories and initial nets
   (tests/golden/cpu_band_c3mem.json);
-* the same gate for C4's arithmetic (8 x 1M lanes with the per-step average-policy
-  exchange), emulated on one GPU by an engine group.
+* the same gate for C4's arithmetic (8 x 1M lanes in 64 pipelined slices, the average-policy
+  nets exchanged after every slice), emulated on one GPU by an engine group.
 """
 import json
 import os
@@ -227,30 +227,37 @@ def test_c3_sliced_learns_within_the_cpu_seed_band(pkg):
 
 
 def test_c4_emulated_learns_within_the_cpu_seed_band(pkg):
-    """C4's arithmetic on one GPU: 8 shards of 1,048,576 lanes (C3's memories each, 16 slices),
-    the average-policy nets exchanged after every step (W0 + mean of the shards' deltas: the
-    RCCL exchange of bench.py --gpus 8, done on device by an engine group; the group runs its
-    slices with lag 1, the ranks' engines with lag 2).  Exploitability at equal TOTAL hands
-    against the CPU band.  Each step is 8.4M hands and one exchange, so the first steps learn
-    slower per hand than one learner; from 33.5M hands on (4 exchanges) the bar is the C3 one:
-    |GPU mean - CPU mean| <= 2 sigma and GPU mean <= CPU mean + 1 sigma.  Measured
-    (profiles/r03_exploit_c4_emulated_slices.json): 1.34 +- 0.12 at 33.5M, 1.19 +- 0.08 at 67M
-    against the CPU's 1.22 +- 0.24 at 32M; without slices (round 2) 1.68 +- 0.40 at 33M."""
+    """C4's arithmetic on one GPU, as bench.py --gpus 8 runs it (bench.CONFIGS["c4"]): 8 shards of
+    1,048,576 lanes (C3's memories each) in 64 pipelined slices (slice_lag 2), the average-policy
+    nets exchanged after EVERY slice -- W0 + 2 x the mean of the shards' deltas, the rank path's
+    arithmetic (tests/test_gpu_exchange.py shows the ranks equal to a group bit for bit) -- done on
+    device by an engine group.  Exploitability at equal TOTAL hands against the CPU band, from the
+    first checkpoint (one step = 8.4M hands) to 8 steps (67M), with the C3 bar:
+    |GPU mean - CPU mean| <= 2 sigma and GPU mean <= CPU mean + 1 sigma (8 seeds each side).
+    Measured (profiles/r04_exploit_c4_slice_exchange.json): 1.526 +- 0.156 at 8.4M (the bar 1.538),
+    1.355 at 16.8M, 1.238, 1.155 at 33.5M, 1.12 at 67M, no frozen learner to 100M; round 3's
+    once-per-step exchange: 1.93 at 8.4M, in the band only from 33.5M."""
+    import bench
+    c4 = bench.CONFIGS["c4"]
     band = _band()
     cpu = {int(h): np.array(v) for h, v in band["curves_by_hands"].items()}
-    R, lanes = 8, 1_048_576
-    checkpoints = (4, 6, 8)                        # steps of 8 x 1,048,576 hands
+    R, lanes, K = 8, c4["n_lanes"], c4["slices"]
+    assert (K, c4["slice_lag"], c4["xchg_every"], c4["xchg_gain"]) == (64, 2, 1, 2.0)
+    checkpoints = (1, 2, 3, 4, 8)                  # steps of 8 x 1,048,576 hands
     gpu = {c: [] for c in checkpoints}
-    for s in range(4):
-        g = pkg.engine.EngineGroup(R, n_lanes=lanes, rl_capacity=C3["rl_capacity"],
-                                   sl_capacity=C3["sl_capacity"], seed=1234 + 1000 * s,
-                                   init_seed=1000 * s, avg_ar=True, slices=16)
+    for s in range(8):
+        g = pkg.engine.EngineGroup(R, n_lanes=lanes, rl_capacity=c4["rl_capacity"], sl_capacity=c4["sl_capacity"],
+                                   seed=1234 + 1000 * s, init_seed=1000 * s, slices=K, slice_lag=2)
+        g.set_exchange(pkg.native.XCHG_AR, every=c4["xchg_every"], scale=c4["xchg_gain"] / R)
         g.average_ar()                             # the common start: replica 0's nets
         for k in range(1, checkpoints[-1] + 1):
             g.step()
             if k in gpu:
                 gpu[k].append(g.exploitability(0)["exploitability"])
         assert g.stats()["hands"] == checkpoints[-1] * R * lanes
+        # one AR net: every replica holds the exchanged nets
+        w0 = g.replicas[0].get_weights(0, 0)
+        assert all(np.array_equal(w0, e.get_weights(0, 0)) for e in g.replicas[1:])
         g.close()
         del g
         torch.cuda.empty_cache()
