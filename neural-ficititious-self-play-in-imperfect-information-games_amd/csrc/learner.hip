@@ -469,11 +469,14 @@ struct LearnPlan {
   std::vector<Segment> seg[2];
   int64_t it0[2];
   FinalArgs F;
+  nfsp_engine::Sched hs;     // the schedules after this call (commit_plan publishes them)
 };
 
-int plan_update(nfsp_engine* e, const EngineDev& h, LearnPlan& L) {
+// The learner call's plan from the rollout's insert counts and the host's schedule mirror.
+// Leaves the engine untouched: commit_plan(e, L) adopts it once every plan of the call (a
+// group's replicas) has succeeded, so a failed plan changes no replica's schedules.
+int plan_update(const nfsp_engine* e, const EngineDev& h, LearnPlan& L) {
   const nfsp_engine_cfg& cfg = e->cfg;
-  e->learn_tag++;
   PrepArgs& P = L.P;
   P = PrepArgs{};
   P.M = e->M;
@@ -485,7 +488,7 @@ int plan_update(nfsp_engine* e, const EngineDev& h, LearnPlan& L) {
   P.E = cfg.epochs;
   P.k0 = (uint32_t)cfg.seed;
   P.k1 = (uint32_t)(cfg.seed >> 32);
-  P.tag = e->learn_tag;
+  P.tag = e->learn_tag + 1;
   P.lr_ar = cfg.lr_ar;
   P.quirks = cfg.quirks;
   L.maxU = L.maxUbr = L.maxSL = 0;
@@ -505,8 +508,6 @@ int plan_update(nfsp_engine* e, const EngineDev& h, LearnPlan& L) {
     L.maxU = pl.U > L.maxU ? pl.U : L.maxU;
     L.maxUbr = pl.U_br > L.maxUbr ? pl.U_br : L.maxUbr;
     L.maxSL = pl.n_sl > L.maxSL ? pl.n_sl : L.maxSL;
-    e->last_U[a] = pl.U;
-    e->last_Ubr[a] = pl.U_br;
   }
   FinalArgs& F = L.F;
   F = FinalArgs{};
@@ -557,14 +558,24 @@ int plan_update(nfsp_engine* e, const EngineDev& h, LearnPlan& L) {
     F.tcount[a] = tc;
     F.syncs[a] = syncs;
     F.eps[a] = eps;
-    e->hs.iteration[a] = it;
-    e->hs.target_count[a] = tc;
-    e->hs.target_syncs[a] = syncs;
-    e->hs.epsilon[a] = eps;
+    L.hs.iteration[a] = it;
+    L.hs.target_count[a] = tc;
+    L.hs.target_syncs[a] = syncs;
+    L.hs.epsilon[a] = eps;
     F.temp[a] = 1.0 / (1.0 + 0.02 * sqrt((double)it));
     F.lr[a] = (float)(cfg.lr_br / (1.0 + 0.003 * sqrt((double)it)));
   }
   return NFSP_OK;
+}
+
+void commit_plan(nfsp_engine* e, const LearnPlan& L) {
+  e->learn_tag = L.P.tag;
+  e->hs = L.hs;
+  for (int a = 0; a < 2; ++a) {
+    e->last_U[a] = L.P.A[a].U;
+    e->last_Ubr[a] = L.P.A[a].U_br;
+  }
+  e->pending_update = false;
 }
 
 int launch_br_prep(nfsp_engine* e, const LearnPlan& L, hipStream_t s) {
@@ -677,7 +688,7 @@ static int update_impl(nfsp_engine* e, bool pipelined, int par, bool snap_after)
   LearnPlan L;
   int rc = plan_update(e, h, L);
   if (rc != NFSP_OK) return rc;
-  e->pending_update = false;
+  commit_plan(e, L);
   // the cross-shard exchange after this call's AR chain (nfsp_engine_set_exchange)
   const bool xchg = e->xchg_every > 0 && (++e->xchg_calls) % e->xchg_every == 0;
   if (pipelined && snap_after)         // the rollout two slices on acts with this epsilon
@@ -1016,9 +1027,9 @@ static int group_update(nfsp_group* g) {
     maxUbr = L[r].maxUbr > maxUbr ? L[r].maxUbr : maxUbr;
     maxSL = L[r].maxSL > maxSL ? L[r].maxSL : maxSL;
   }
-  // every plan succeeded: the rollouts are consumed (a failed plan leaves all of them
-  // pending, so the replicas stay in step)
-  for (int r = 0; r < R; ++r) g->eng[r]->pending_update = false;
+  // every plan succeeded: the rollouts are consumed and the schedules advance (a failed
+  // plan leaves every replica as it was -- pending, schedules untouched -- so they stay in step)
+  for (int r = 0; r < R; ++r) commit_plan(g->eng[r], L[r]);
   // ---- tables: prep / final args per replica; the AR chains (2R workgroups, one launch);
   // per BR round k the targets and the chain of every (replica, agent) with a k-th segment
   std::vector<ChainJob> ar_jobs;

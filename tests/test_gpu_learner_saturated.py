@@ -13,13 +13,13 @@ itself against the oracle:
 * an engine whose AR nets' layer 2 is scaled x60 before a learner call (saturated softmax on
   most observations), stopped after k updates (nfsp_engine_set_update_limit) for every k;
 * resynchronised replay: update k replayed by the oracle from the ENGINE's weights after k
-  updates, compared with the engine after k + 1.  Bar: every update whose samples keep every
-  p away from a clip bound (relative distance > 4e-7, ~6 ulps at 1 - 1e-7) agrees within 1e-5
-  (relative to max(1, |w|)); an update that does not is a clip-mask flip, and is listed;
+  updates, compared with the engine after k + 1.  Bar: every single update agrees within 1e-5
+  (relative to max(1, |w|)), although nearly every one has a p within 4e-7 (relative; ~3 ulps
+  at 1 - 1e-7) of a clip bound -- the regime is the saturated one (measured: <= 2.1e-7);
 * free replay (no resynchronisation): every onset of a > 1e-4 divergence lies in an update
   with a p within 4e-7 (relative) of a clip bound -- a clip-mask flip -- or a hidden
   pre-activation within 1e-7 of zero (the ReLU kink of test_gpu_learner_divergence.py).
-The log goes to profiles/r04_learner_saturated.txt (tools/gpu_tests.sh copies the -s output)."""
+The -s output of a run is kept as profiles/r04_learner_saturated.txt."""
 import numpy as np
 import pytest
 import torch
@@ -57,7 +57,7 @@ def _rel(a, b):
     return float((np.abs(a - b) / np.maximum(1.0, np.abs(b))).max())
 
 
-def test_saturated_ar_updates_agree_except_at_clip_flips(pkg):
+def test_saturated_ar_single_updates_agree_and_divergence_starts_at_clip_flips(pkg):
     eng0 = _engine_after(pkg, 0)
     st0, state = _snapshot(eng0)
     cfg = _oracle_cfg(eng0.cfg)
@@ -72,7 +72,6 @@ def test_saturated_ar_updates_agree_except_at_clip_flips(pkg):
         w_at[k] = [e.get_weights(a, 0) for a in (0, 1)]
         del e
         torch.cuda.empty_cache()
-    # how saturated: the share of the first update's samples with a clipped output
     sat = []
     resync, flips = [], []
     for a in (0, 1):
@@ -83,7 +82,6 @@ def test_saturated_ar_updates_agree_except_at_clip_flips(pkg):
             resync.append((a, k, d, closest.get(mbs[a][k][0], np.inf), bool(amb)))
             if d > 1e-5:
                 flips.append((a, k, d))
-                assert amb, ("an update left the oracle without a p near a clip bound", resync[-1])
         # the free replay from the start
         w = w_at[0][a]
         prev = 0.0
@@ -99,8 +97,8 @@ def test_saturated_ar_updates_agree_except_at_clip_flips(pkg):
             prev = d
     print("resynchronised single updates: agent, update, max rel |oracle - engine|, closest p to a clip "
           "bound (relative), ambiguous:", [(a, k, f"{d:.1e}", f"{c:.1e}", m) for a, k, d, c, m in resync])
-    print("updates past 1e-5 (clip-mask flips):", flips)
     print("free-replay divergence onsets (agent, update, rel diff, cause):", sat)
+    assert not flips, ("single updates past 1e-5", flips)
     # the regime is the saturated one: outputs at the clip bounds are common
     near = [c for _, _, _, c, _ in resync]
     assert min(near) < 1e-3

@@ -152,6 +152,27 @@ def test_pipelined_slices_act_with_the_nets_two_slices_back(pkg, K):
     _check_slice_lanes(eng, seed, _sample_lanes(eng.slice_lanes, 48, 20 + K), before, w, eps)
 
 
+def test_pipelined_snapshot_keeps_the_epsilon_its_slice_acted_with(pkg):
+    """The epsilon half of the snapshot: a setting where epsilon has NOT
+    decayed to ~0 between the slices (eps 0.9, eta 1 so every decision is an eps-greedy BR one,
+    an update per ~1,500 RL inserts so eps / iteration falls slowly).  The last slice of the
+    first step is replayed with snapshot (K - 1) & 1's nets and epsilon; the epsilon after the
+    step, which a snapshot overwritten by the last slice's own learner call would report, differs
+    and would change ~2% of the draws."""
+    seed, K = 6060, 8
+    eng = pkg.engine.SelfPlayEngine(seed=seed, init_seed=3, slices=K, slice_lag=2, n_lanes=4096,
+                                    rl_capacity=20_000, sl_capacity=20_000, inserts_per_update=2048,
+                                    epsilon=0.9, eta=1.0)
+    eng.step()
+    st = eng.stats()
+    w, eps = eng.snapshot((K - 1) & 1)
+    assert 1e-3 < min(eps) and max(eps) < 0.9                   # decayed, but far from 0
+    assert st["epsilon"][0] < 0.5 * eps[0]                     # the step's last learner moved it
+    assert eng.last_slice() == ((K - 1) * eng.slice_lanes, 0)
+    before = tuple(int(st["rl_total"][p] - st["last_rl"][p]) for p in (0, 1))
+    _check_slice_lanes(eng, seed, range(eng.slice_lanes), before, w, eps)
+
+
 def test_kuhn_textbook_pipelined_slices_replay_on_the_oracle(pkg):
     """bench.py's C5-textbook form (Kuhn, NFSP_TEXTBOOK_MSE, 16 pipelined slices) at 262,144
     lanes: the last slice of the second step replays bit-exact with the snapshot it acted with
