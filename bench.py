@@ -762,7 +762,7 @@ def main():
     xchg_ms = k_ms.get("ar_exchange") if avg is not None and k_launches.get("ar_exchange") else None
     if avg is not None:
         out["ar_allreduce"] = {"calls": avg.calls, "calls_timed_pass": x1 - x0, "bytes_per_call": avg.bytes_per_call,
-                               "backend": args.dist_backend, "transport": avg.transport,
+                               "backend": args.dist_backend, "transport": avg.transport, "fallback": avg.fallback,
                                "every_slices": args.xchg_every, "gain": args.xchg_gain,
                                "ms_per_call_event_timed": xchg_ms,
                                "ms_per_call_is": "HIP events on the AR stream around delta + all-reduce + "

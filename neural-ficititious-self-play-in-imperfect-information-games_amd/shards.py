@@ -131,23 +131,39 @@ class AvgPolicyExchange:
         self.comm = None
         self._fn = None
         L = engine.L
+        self.fallback = None
         if self.transport == "rccl":
+            # rank 0's id to every rank; each rank reports whether its RCCL setup worked, and
+            # unless all did, every rank falls back to the host transport together (a job
+            # that cannot build the communicator still runs, its exchange host-synchronised)
             uid = (C.c_uint8 * 128)()
+            ok = 1
             if self.rank == src:
-                native.check(L.nfsp_rccl_unique_id(uid), "nfsp_rccl_unique_id")
+                ok = int(L.nfsp_rccl_unique_id(uid) == native.OK)
             dev = "cuda" if backend == "nccl" else "cpu"
-            t = torch.tensor(list(uid), dtype=torch.uint8, device=dev)
+            t = torch.tensor(list(uid) + [ok], dtype=torch.uint8, device=dev)
             dist.broadcast(t, src=src)
-            uid = (C.c_uint8 * 128)(*t.cpu().tolist())
+            vals = t.cpu().tolist()
+            uid = (C.c_uint8 * 128)(*vals[:128])
             comm = native.P()
-            native.check(L.nfsp_rccl_comm_create(uid, self.world, self.rank, torch.cuda.current_device(),
-                                                  C.byref(comm)), "nfsp_rccl_comm_create")
-            self.comm = comm
-            engine.set_exchange(self.every, self.gain / self.world, comm=comm)
-        elif self.transport == "host":
+            rc = native.EINVAL
+            if vals[128]:
+                rc = L.nfsp_rccl_comm_create(uid, self.world, self.rank, torch.cuda.current_device(), C.byref(comm))
+            good = torch.tensor([1 if rc == native.OK else 0], dtype=torch.int32, device=dev)
+            dist.all_reduce(good, op=dist.ReduceOp.MIN)
+            if int(good.item()) == 1:
+                self.comm = comm
+                engine.set_exchange(self.every, self.gain / self.world, comm=comm)
+            else:
+                if rc == native.OK:
+                    L.nfsp_rccl_comm_destroy(comm)
+                self.fallback = "rccl setup failed on some rank: " + L.nfsp_last_error().decode()
+                print(f"AvgPolicyExchange: {self.fallback}; using the host transport", file=sys.stderr)
+                self.transport = "host"
+        if self.transport == "host":
             self._fn = native.EXCHANGE_FN(self._host_sum)
             engine.set_exchange(self.every, self.gain / self.world, fn=self._fn)
-        else:
+        elif self.transport != "rccl":
             raise ValueError(f"unknown transport {transport!r}")
 
     def _host_sum(self, _user, ptr, n):
