@@ -57,6 +57,16 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
+# Hardware queues per process (read when HIP initialises, so before torch is imported).  An
+# engine runs 4 streams that must not share a queue: a rollout queued behind a 1 ms SGD chain
+# kernel breaks the slices' pipelining.  HIP's default of 4 queues is enough while the engine's
+# streams are the process's only busy ones, but a process group (torch's NCCL streams, the
+# exchange's RCCL communicator) adds streams, and with 4 queues the ctx stream landed on agent 0's
+# BR queue: C4's per-rank line with the exchange ran 179.0 ms per step, 168.9 with 8 queues and
+# 168.7 with 16; C3 alone 166.9 / 166.7 / 167.3 (`tools/hwq_probe.sh`).
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
 CONFIGS = {
     # C3 advances its 1M lanes in 16 slices of 65,536 (include/nfsp.h cfg.slices), pipelined
     # (cfg.slice_lag 2: a slice acts with the nets its predecessor's predecessor's learner left,

@@ -278,6 +278,9 @@ struct nfsp_engine {
   void* xchg_comm = nullptr;         // RCCL communicator, or
   nfsp_exchange_fn xchg_fn = nullptr;  // the host transport
   void* xchg_user = nullptr;
+  bool xchg_pending = false;         // a pipelined call's exchange, enqueued by the next call
+  int xchg_pend_par = 0;             //   (or the step's end), with the AR snapshot it feeds
+  bool xchg_pend_snap = false;
   // host mirror of the schedules (agent/agent.py:245-253, 266-273): plan_update computes them
   // in the reference's double arithmetic; k_finalize publishes them to EngineDev for the stats
   struct Sched {

@@ -670,6 +670,26 @@ int launch_br_chain(const ChainArgs& C, int blocks, unsigned quirks, bool loss_l
 
 }  // namespace
 
+// The exchange a pipelined learner call left pending (nfsp_engine_set_exchange), enqueued on
+// the AR stream behind that call's AR chain, then the AR snapshot it feeds and its event.
+static int flush_exchange(nfsp_engine* e) {
+  if (!e->xchg_pending) return NFSP_OK;
+  e->xchg_pending = false;
+  int rc;
+  {
+    KTimer kx(e, KT_XCHG, e->s_ar);
+    if ((rc = exchange_enqueue(e, e->s_ar)) != NFSP_OK) return rc;
+  }
+  if (e->xchg_pend_snap) {
+    float* snap = e->snap + (size_t)e->xchg_pend_par * 6 * nn::NP;
+    for (int a = 0; a < 2; ++a)
+      NFSP_HIP(hipMemcpyAsync(snap + (a * 3 + 0) * nn::NP, e->w + (a * 3 + 0) * nn::NP,
+                              sizeof(float) * nn::NP, hipMemcpyDeviceToDevice, e->s_ar));
+    NFSP_HIP(hipEventRecord(e->snap_ev[e->xchg_pend_par][0], e->s_ar));
+  }
+  return NFSP_OK;
+}
+
 // One learner call for the pending rollout.  par: the learner-buffer set (slice parity; 0
 // unless cfg.slice_lag 2).  pipelined: leave the chains running (no join into the ctx
 // stream; each BR stream publishes its agent's results itself), and when snap_after, copy
@@ -711,68 +731,95 @@ static int update_impl(nfsp_engine* e, bool pipelined, int par, bool snap_after)
     NFSP_LAUNCHED("k_finalize");
   }
   float* snap = e->snap + (size_t)par * 6 * nn::NP;
-  // ---- AR chains (both agents, one launch) on their own stream
-  NFSP_HIP(hipStreamWaitEvent(e->s_ar, fork, 0));
-  if (L.maxU > 0) {
-    ChainArgs C{};
-    C.B = cfg.batch;
-    C.E = cfg.epochs;
-    for (int a = 0; a < 2; ++a) {
-      C.job[a] = ar_job(e, L, a);
-      if (snap_after && !xchg) C.job[a].snap_to = snap + (a * 3 + 0) * nn::NP;   // written by the chain
-    }
-    KTimer kc(e, KT_CHAIN_AR, e->s_ar);
-    if ((rc = launch_chain_ar(C, 2, e->log_loss, e->s_ar)) != NFSP_OK) return rc;
-  }
-  if (xchg) {
-    KTimer kx(e, KT_XCHG, e->s_ar);
-    if ((rc = exchange_enqueue(e, e->s_ar)) != NFSP_OK) return rc;
-  }
-  if (snap_after && (xchg || L.maxU == 0))   // the AR nets as they are now (exchanged)
-    for (int a = 0; a < 2; ++a)
-      NFSP_HIP(hipMemcpyAsync(snap + (a * 3 + 0) * nn::NP, e->w + (a * 3 + 0) * nn::NP,
-                              sizeof(float) * nn::NP, hipMemcpyDeviceToDevice, e->s_ar));
-  if (snap_after) NFSP_HIP(hipEventRecord(e->snap_ev[par][0], e->s_ar));
   // diagnostic (NFSP_LEARNER_SERIAL=1): BR work waits for the AR chains, to time them alone
   static const bool serial_ar = getenv("NFSP_LEARNER_SERIAL") && atoi(getenv("NFSP_LEARNER_SERIAL"));
   hipEvent_t ar_done = fork;
-  if (serial_ar) {
-    ar_done = take_event(e);
-    NFSP_HIP(hipEventRecord(ar_done, e->s_ar));
-  }
-  // ---- BR: per agent on its own stream, segments between target syncs = targets + chain
-  for (int a = 0; a < 2; ++a) {
-    hipStream_t sa = e->s_br[a];
-    NFSP_HIP(hipStreamWaitEvent(sa, serial_ar ? ar_done : fork_br, 0));
-    KTimer kspan(e, KT_BR_STREAM0 + a, sa);     // this agent's BR stream, end to end
-    for (size_t gi = 0; gi < L.seg[a].size(); ++gi) {
-      const Segment& sg = L.seg[a][gi];
-      {
-        KTimer kt2(e, KT_TARGETS, sa);
-        k_br_targets<<<(unsigned)(sg.v - sg.u), 256, 0, sa>>>(nullptr, br_target_job(e, L, a, sg),
-                                                                cfg.batch, cfg.epochs, cfg.gamma,
-                                                                cfg.quirks, cfg.lr_br);
-      }
-      NFSP_LAUNCHED("k_br_targets");
+  // ---- AR chains (both agents, one launch) on their own stream.  With the exchange on and
+  // the slices pipelined, this call's exchange (and the AR snapshot it feeds) is enqueued by
+  // the NEXT call, after its prep and BR chains and right before its AR chain (or at the
+  // step's end): an exchange may hold the host until the AR stream reaches it (RCCL's world-1
+  // path synchronises the stream), and this way the host has enqueued everything the other
+  // streams need before it can wait -- the AR stream's next chain needs the exchange anyway.
+  auto ar_part = [&]() -> int {
+    int r;
+    if (pipelined && (r = flush_exchange(e)) != NFSP_OK) return r;
+    NFSP_HIP(hipStreamWaitEvent(e->s_ar, fork, 0));
+    if (L.maxU > 0) {
       ChainArgs C{};
       C.B = cfg.batch;
       C.E = cfg.epochs;
-      C.job[0] = br_chain_job(e, a, sg);
-      if (snap_after && gi + 1 == L.seg[a].size())            // the last segment writes the snapshot
-        C.job[0].snap_to = snap + (a * 3 + 1) * nn::NP;
-      KTimer kc(e, KT_CHAIN_BR, sa);
-      if ((rc = launch_br_chain(C, 1, cfg.quirks, e->log_loss, sa)) != NFSP_OK) return rc;
+      for (int a = 0; a < 2; ++a) {
+        C.job[a] = ar_job(e, L, a);
+        if (snap_after && !xchg) C.job[a].snap_to = snap + (a * 3 + 0) * nn::NP;   // written by the chain
+      }
+      KTimer kc(e, KT_CHAIN_AR, e->s_ar);
+      if ((r = launch_chain_ar(C, 2, e->log_loss, e->s_ar)) != NFSP_OK) return r;
     }
-    if (pipelined) {                   // this agent's learner results, after its chain
-      k_finalize<0><<<1, 64, 0, sa>>>(L.F, nullptr, 2 << a);
-      NFSP_LAUNCHED("k_finalize");
+    if (xchg) {
+      e->xchg_pending = true;
+      e->xchg_pend_par = par;
+      e->xchg_pend_snap = snap_after;
+      if (!pipelined && (r = flush_exchange(e)) != NFSP_OK) return r;
+    } else if (snap_after) {
+      if (L.maxU == 0)                 // no AR chain this call: copy the nets as they are
+        for (int a = 0; a < 2; ++a)
+          NFSP_HIP(hipMemcpyAsync(snap + (a * 3 + 0) * nn::NP, e->w + (a * 3 + 0) * nn::NP,
+                                  sizeof(float) * nn::NP, hipMemcpyDeviceToDevice, e->s_ar));
+      NFSP_HIP(hipEventRecord(e->snap_ev[par][0], e->s_ar));
     }
-    if (snap_after) {
-      if (L.seg[a].empty())             // no BR chain this call: copy the net as it is
-        NFSP_HIP(hipMemcpyAsync(snap + (a * 3 + 1) * nn::NP, e->w + (a * 3 + 1) * nn::NP,
-                                sizeof(float) * nn::NP, hipMemcpyDeviceToDevice, sa));
-      NFSP_HIP(hipEventRecord(e->snap_ev[par][1 + a], sa));
+    if (serial_ar) {
+      ar_done = take_event(e);
+      NFSP_HIP(hipEventRecord(ar_done, e->s_ar));
     }
+    return NFSP_OK;
+  };
+  // ---- BR: per agent on its own stream, segments between target syncs = targets + chain
+  auto br_part = [&]() -> int {
+    int r;
+    for (int a = 0; a < 2; ++a) {
+      hipStream_t sa = e->s_br[a];
+      NFSP_HIP(hipStreamWaitEvent(sa, serial_ar ? ar_done : fork_br, 0));
+      KTimer kspan(e, KT_BR_STREAM0 + a, sa);     // this agent's BR stream, end to end
+      for (size_t gi = 0; gi < L.seg[a].size(); ++gi) {
+        const Segment& sg = L.seg[a][gi];
+        {
+          KTimer kt2(e, KT_TARGETS, sa);
+          k_br_targets<<<(unsigned)(sg.v - sg.u), 256, 0, sa>>>(nullptr, br_target_job(e, L, a, sg),
+                                                                  cfg.batch, cfg.epochs, cfg.gamma,
+                                                                  cfg.quirks, cfg.lr_br);
+        }
+        NFSP_LAUNCHED("k_br_targets");
+        ChainArgs C{};
+        C.B = cfg.batch;
+        C.E = cfg.epochs;
+        C.job[0] = br_chain_job(e, a, sg);
+        if (snap_after && gi + 1 == L.seg[a].size())            // the last segment writes the snapshot
+          C.job[0].snap_to = snap + (a * 3 + 1) * nn::NP;
+        KTimer kc(e, KT_CHAIN_BR, sa);
+        if ((r = launch_br_chain(C, 1, cfg.quirks, e->log_loss, sa)) != NFSP_OK) return r;
+      }
+      if (pipelined) {                   // this agent's learner results, after its chain
+        k_finalize<0><<<1, 64, 0, sa>>>(L.F, nullptr, 2 << a);
+        NFSP_LAUNCHED("k_finalize");
+      }
+      if (snap_after) {
+        if (L.seg[a].empty())             // no BR chain this call: copy the net as it is
+          NFSP_HIP(hipMemcpyAsync(snap + (a * 3 + 1) * nn::NP, e->w + (a * 3 + 1) * nn::NP,
+                                  sizeof(float) * nn::NP, hipMemcpyDeviceToDevice, sa));
+        NFSP_HIP(hipEventRecord(e->snap_ev[par][1 + a], sa));
+      }
+    }
+    return NFSP_OK;
+  };
+  // pipelined with the exchange: the BR chains first (they never wait for an exchange), then
+  // the previous call's exchange and this call's AR chain
+  const bool br_first = pipelined && e->xchg_every > 0 && !serial_ar;
+  if (br_first) {
+    if ((rc = br_part()) != NFSP_OK) return rc;
+    if ((rc = ar_part()) != NFSP_OK) return rc;
+  } else {
+    if ((rc = ar_part()) != NFSP_OK) return rc;
+    if ((rc = br_part()) != NFSP_OK) return rc;
   }
   e->pool.push_back(fork);
   e->pool.push_back(fork_br);
@@ -833,6 +880,7 @@ int step_pipelined(nfsp_engine* e) {
       return rc;
     if ((rc = update_impl(e, true, par, j + 2 < K)) != NFSP_OK) return rc;
   }
+  if ((rc = flush_exchange(e)) != NFSP_OK) return rc;    // the last slice's
   return join_streams(e);
 }
 }  // namespace eng
