@@ -100,6 +100,7 @@ int rccl_fail(ncclResult_t r, const char* what) {
 namespace nfsp {
 namespace eng {
 int exchange_enqueue(nfsp_engine* e, hipStream_t s) {
+  NFSP_REQUIRE(e->xchg_comm || e->xchg_fn, "the exchange has no transport");
   const unsigned nb = nfsp_blocks(2 * nn::NP, 256);
   k_xchg_delta<<<nb, 256, 0, s>>>(e->w, e->xchg_w0, e->xchg_buf);
   NFSP_LAUNCHED("k_xchg_delta");
@@ -127,7 +128,8 @@ extern "C" int nfsp_engine_set_exchange(nfsp_engine* e, int every, float scale, 
   NFSP_REQUIRE(every >= 0, "every must be >= 0");
   NFSP_REQUIRE(every == 0 || ((rccl_comm != nullptr) != (fn != nullptr)),
                "exactly one transport: an RCCL communicator or a host callback");
-  NFSP_REQUIRE(!e->pending_update, "set the exchange between steps (a rollout is pending)");
+  NFSP_REQUIRE(!e->pending_update && !e->xchg_pending,
+               "set the exchange between steps (a rollout or an exchange is pending)");
   if (every > 0 && !e->xchg_w0) {
     for (float** p : {&e->xchg_w0, &e->xchg_buf}) {
       NFSP_HIP(hipMalloc((void**)p, sizeof(float) * 2 * nn::NP));
