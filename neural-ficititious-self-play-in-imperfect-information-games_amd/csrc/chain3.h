@@ -3,6 +3,7 @@
 // The two are compiled with different scheduler flags (__graft_entry__.FILE_FLAGS).
 #pragma once
 #include <atomic>
+#include <type_traits>
 
 #include "engine_internal.h"
 
@@ -82,6 +83,29 @@ __device__ inline float sum_x16(float x) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
+// Sums over the 32 samples held by the loss lanes (k_chain3's `ls` layout: every sample in 2
+// lanes), in every lane, added in exactly the round-3 chain's order (it held sample c in lane
+// c of rows 0 / 1 and 16 + c in rows 2 / 3, summed each row by DPP row_ror 8, 4, 2, 1, then
+// the two halves): pairs s, s ^ 8 (rows g, g ^ 2), s ^ 4 (lanes c, c ^ 8), s ^ 2, s ^ 1 (quad
+// permutes), then samples 0-15 + 16-31 (lanes c, c ^ 4).  a + b == b + a bit for bit, so
+// every level is the round-3 level, and the 32-sample totals are bit-identical to it.
+template <int CTRL>
+__device__ inline float dpp_bc(float x) {           // every lane has a source: bound_ctrl on
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, true));
+}
+__device__ inline float tot_rows(float x) {        // levels 2 .. 5, after the rows' level 1
+  x = x + dpp_bc<0x128>(x);
+  x = x + dpp_bc<0x4E>(x);
+  x = x + dpp_bc<0xB1>(x);
+  return x + dpp_bc<0x124>(x);
+}
+__device__ inline float tot32(float x) { return tot_rows(sum_x32(x)); }
+// two totals at once: rows 0 / 1 get a's, rows 2 / 3 b's
+__device__ inline float tot32_pair(float a, float b) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  return tot_rows(__uint_as_float(r[0]) + __uint_as_float(r[1]));
+}
+
 // ---------------------------------------------------------------------------
 // k_chain3: the SGD chain on bf16 matrix cores with exact-f32 operands.
 //
@@ -105,7 +129,8 @@ __device__ inline float sum_x16(float x) {
 //     publishes it.  The dW1 operand X^T is the same fa image read transposed
 //     (ds_read_b64_tr_b16), so a record is the fa image and the targets, 2,560 B;
 //   * one barrier per step (the 4 waves' layer-2 partials); all other exchange is
-//     wave-private (LDS dm / w2t) or cross-lane (DPP, permlane).
+//     wave-private (LDS w2t) or cross-lane (DPP, permlane).  The loss gradients reach the
+//     backward's sample-major layout by DPP row broadcasts fused into its FMAs (bwd_dpp).
 // ---------------------------------------------------------------------------
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
@@ -115,13 +140,12 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 static __device__ unsigned long long g_chain_stamps[8][4][10];
 #endif
 
-// Stores are unconditional: lanes whose copy is redundant (the odd lane rows of po / dm, the
-// rows g > 0 of w2t, the lanes past a record quarter) write to sink rows nobody reads, so
-// the loop has no exec-mask branches.
+// Stores are unconditional: lanes whose copy is redundant (the rows g > 0 of w2t, the lanes
+// past a record quarter) write to sink rows nobody reads, so the loop has no exec-mask
+// branches.
 struct Chain3Smem {
   float po[2][4][64][4];     // per-wave partial layer-2 outputs by sample (rows 0..31 used),
                              // double-buffered by step parity
-  float dm[4][3][64];        // wave-private: dL/dz2 of the 32 samples, by output (32..63: sink)
   float4 w2t[4][64];         // wave-private: W2[h][0..2] of the slice (rows 0..15: the layer-2
                              // weights live here, each component written by the lanes owning it)
   float b2s[4][4];           // wave-private: b2
@@ -245,6 +269,46 @@ __device__ inline floatx4 mfma3t(bf16x8 ahi, bf16x8 amid, bf16x8 alo, bf16x8 b) 
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, b, z, 0, 0, 0);
 }
 
+// The backward of one sample slot j of the sample-major layout (lane (g, c) holds samples
+// 4g + j (j < 4) and 16 + 4g + j - 4 (j >= 4), hidden 16w + c), with the loss gradients
+// x0..x2 of that sample taken from lane j of the lane's own row by DPP row_newbcast, fused
+// into the FMAs (the loss lanes are laid out so that lane j of row g holds exactly that
+// sample, see `ls` in k_chain3):
+//   g2_k += h * x_k  (k = 0..2),   dh = fma(x2, W2_2, fma(x0, W2_0, x1 * W2_1))
+// the same operations in the same order as the round-3 chain (which read the x_k back from
+// an LDS copy of dL/dz2 and compiled (x0 W2_0 + x1 W2_1) + x2 W2_2 to exactly those fmas).  The compiler does not fuse a DPP
+// move into v_fmac_f32, hence asm.  Hazard: a DPP source read >= 2 wait states after the
+// VALU write of that register; the x_k are written before slot 0's statement, which starts
+// with s_nop 1 (slot j + 1 reads slot j's g2 sums, so slot 0's statement comes first).  Not
+// volatile: a volatile statement bounds the scheduler's regions, and the DPP chains of the
+// totals (tot32) then lose the instructions that hide their hazards.
+#define NFSP_BWD_DPP(L, NOP, OPG, CG)                                                       \
+  asm(NOP                                                                                 \
+               OPG " %0, %4, %7 row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n\t"            \
+               OPG " %1, %5, %7 row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n\t"            \
+               OPG " %2, %6, %7 row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n\t"            \
+               "v_mul_f32_dpp %3, %5, %9 row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n\t"  \
+               "v_fmac_f32_dpp %3, %4, %8 row_newbcast:" #L " row_mask:0xf bank_mask:0xf\n\t" \
+               "v_fmac_f32_dpp %3, %6, %10 row_newbcast:" #L " row_mask:0xf bank_mask:0xf"     \
+               : CG(g0), CG(g1), CG(g2), "=&v"(dh)                                             \
+               : "v"(x0), "v"(x1), "v"(x2), "v"(h), "v"(W0), "v"(W1), "v"(W2))
+// slot 0 starts the g2 sums (a product, no accumulator register to zero)
+template <int L>
+__device__ inline float bwd_dpp(float& g0, float& g1, float& g2, float x0, float x1, float x2, float h,
+                                float W0, float W1, float W2) {
+  float dh;
+  if constexpr (L == 0) NFSP_BWD_DPP(0, "s_nop 1\n\t", "v_mul_f32_dpp", "=&v");
+  else if constexpr (L == 1) NFSP_BWD_DPP(1, "", "v_fmac_f32_dpp", "+v");
+  else if constexpr (L == 2) NFSP_BWD_DPP(2, "", "v_fmac_f32_dpp", "+v");
+  else if constexpr (L == 3) NFSP_BWD_DPP(3, "", "v_fmac_f32_dpp", "+v");
+  else if constexpr (L == 4) NFSP_BWD_DPP(4, "", "v_fmac_f32_dpp", "+v");
+  else if constexpr (L == 5) NFSP_BWD_DPP(5, "", "v_fmac_f32_dpp", "+v");
+  else if constexpr (L == 6) NFSP_BWD_DPP(6, "", "v_fmac_f32_dpp", "+v");
+  else NFSP_BWD_DPP(7, "", "v_fmac_f32_dpp", "+v");
+  return dh;
+}
+#undef NFSP_BWD_DPP
+
 // RELU: 0 = the AR net (softmax, categorical cross-entropy), 1 = the BR net (ReLU Q head,
 // Huber), 2 = a BR net with a linear Q head (NFSP_EXT_LINEAR_Q, Huber), 3 = linear head with
 // mean squared error (NFSP_EXT_MSE_Q).
@@ -261,7 +325,13 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
   const int l = tid & 63;
   const int g = l >> 4, c = l & 15;
   const int hid = 16 * w + c;
-  const int sl = 16 * (g >> 1) + c;            // this lane's loss sample
+  const int sl = 16 * (g >> 1) + c;            // this lane's layer-2 partial sample (Z1^T)
+  // this lane's loss sample: lane j < 8 of row g holds sample 4g + (j & 3) + 16 (j >> 2), the
+  // samples the row's backward slot j needs (bwd_dpp); lanes 8..15 hold the other row of the
+  // pair's samples, so rows g and g ^ 1 hold the same 16 samples (rows 0 / 1: 0-7, 16-23;
+  // rows 2 / 3: 8-15, 24-31), in an order whose row sums (DPP row_shr 8, 4, 2, 1) agree bit
+  // for bit
+  const int ls = 4 * ((g & 2) | ((g & 1) ^ (c >> 3))) + (c & 3) + 16 * ((c >> 2) & 1);
   float* gw = J.w;
   float wr[8];
 #pragma unroll
@@ -288,19 +358,26 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
   }
   const int T1 = (int)(u1 * spu);
   int t = (int)(u0 * spu);
-  const uint4* recb = reinterpret_cast<const uint4*>(J.rec);
   // this wave's quarter of record p (clamped), into a register / back into ring slot p & 3;
-  // the lanes past the quarter load a duplicate chunk and store it to the sink
+  // the lanes past the quarter load a duplicate chunk and store it to the sink.  The loads go
+  // through a buffer descriptor: the record offset is a scalar, the lane's chunk offset a
+  // loop-invariant VGPR (no 64-bit address arithmetic per step)
   const bool in_q = l < REC_QUARTER;
   const int la = in_q ? l : REC_QUARTER - 1;
+  const int T1c = T1 > 0 ? T1 : 1;
+  const auto rrsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<StepRec*>(J.rec), 0,
+                                                       (int)((size_t)T1c * sizeof(StepRec)), 0x00020000);
+  const int va_off = (REC_QUARTER * w + la) * 16;
   auto issue = [&](int p, uint4& va) {
-    const uint4* src = recb + (size_t)(p < T1 ? p : T1 - 1) * REC_CHUNKS + REC_QUARTER * w;
-    va = src[la];
+    const int pc = p < T1 ? p : T1 - 1;
+    va = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rrsrc, va_off, pc * (int)sizeof(StepRec), 0));
   };
-  auto stash = [&](int p, const uint4& va) {
-    uint4* dst = reinterpret_cast<uint4*>(&sm.ring[p & 3]) + REC_QUARTER * w;
+  // ring slot `slot` (a constant in the unrolled loop): lanes past the quarter store to the sink
+  auto stash_slot = [&](int slot, const uint4& va) {
+    uint4* dst = reinterpret_cast<uint4*>(&sm.ring[slot]) + REC_QUARTER * w;
     *(in_q ? dst + l : &sm.rec_sink[l]) = va;
   };
+  auto stash = [&](int p, const uint4& va) { stash_slot(p & 3, va); };
   // X^T (the dW1 operand, K = samples) by transposed reads of the fa image: in each 16-lane
   // group g, lane c = 4q + p supplies row q = sample 4g + q, columns 4p .. 4p + 3 = inputs
   // 4p .. 4p + 3, i.e. the first 8 bytes of sample 4g + q's chunk of row p; lane c receives
@@ -311,15 +388,14 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
   auto publish = [&]() {   // this wave's W2 rows for its own Z1^T layer 2
     sm.w2t[w][l] = make_float4(W2_0, W2_1, W2_2, 0.f);
   };
-  const int prow = 32 * (g & 1) + sl;          // po / dm row: the sample, or the sink
   const SplitK SK = split_consts();
   // W2 and b2 live in the wave's LDS (w2t rows 0..15, b2s); the cross-lane reductions leave
   // each gradient total in one row of lanes (see the update), and that row owns the value:
   //   row 0: W2[c][0]   row 1: W2[c][2]   row 2: W2[c][1]   row 3: b2[0]  (own1; row 3's total
-  //   is 2 gb2[0], scaled by 1/2 -- exact)        rows 0, 1: b2[1]   rows 2, 3: b2[2]  (own2)
+  //   is 4 gb2[0], scaled by 1/4 -- exact)        rows 0, 1: b2[1]   rows 2, 3: b2[2]  (own2)
   float* const own1 = g == 3 ? &sm.b2s[w][0] : reinterpret_cast<float*>(&sm.w2t[w][c]) + (g == 0 ? 0 : g == 1 ? 2 : 1);
   float* const own2 = &sm.b2s[w][g < 2 ? 1 : 2];
-  const float own1_sc = g == 3 ? 0.5f : 1.0f;
+  const float own1_sc = g == 3 ? 0.25f : 1.0f;
 #ifdef NFSP_CHAIN_STAMPS
   unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_last = 0;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
@@ -330,14 +406,17 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
   // load is consumed inside its own step (nothing loop-carried in registers), and the 4
   // waves share one copy of each record.
   float loss_acc = 0.f;                        // wave 0 lane 0: running epoch loss
-  auto step = [&]() {
+  // PH: t & 3 when the caller knows it at compile time (the loop unrolled by 4), else -1
+  auto step = [&](auto PHC) {
+    constexpr int PH = decltype(PHC)::value;
+    const int slot = PH >= 0 ? PH : (t & 3);
     uint4 va;
     issue(t + 2, va);
-    const StepRec& R = sm.ring[t & 3];
+    const StepRec& R = sm.ring[slot];
     const bf16x8 fa0 = __builtin_bit_cast(bf16x8, R.fa[g][c ^ fsw]);
     const bf16x8 fa1 = __builtin_bit_cast(bf16x8, R.fa[g][(16 + c) ^ fsw]);
     // X^T, read where each chain measured fastest (tools/chain_ab.sh; results identical):
-    // BR right after the barrier, AR after the dm reads.  Beside the fa reads both were
+    // BR right after the barrier, AR after the loss (round 3: after the dm reads).  Beside the fa reads both were
     // slower (BR 0.831 -> 0.90 us, bimodal), as was carrying them from the previous step.
     bf16x8 ba0, ba1;
     const char* const rtr = reinterpret_cast<const char*>(&R.fa[0][0]) + tr_off;
@@ -374,7 +453,7 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
         p1[k] = p1[k] + h1 * W2h[r][k];
       }
     }
-    const int buf = t & 1;
+    const int buf = PH >= 0 ? (PH & 1) : (t & 1);
     float q[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {   // rows g, g ^ 2 (tile halves)
@@ -392,7 +471,7 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
     __builtin_amdgcn_sched_barrier(0);
     const floatx4 zs0 = mfma3(fa0, whi, wmid, wlo);      // Z1: sample 4g+r, hidden 16w+c
     const floatx4 zs1 = mfma3(fa1, whi, wmid, wlo);      //     sample 16+4g+r
-    const float4 tg = R.tg[sl];                          // read before the barrier pins it early
+    const float4 tg = R.tg[ls];                          // read before the barrier pins it early
     __builtin_amdgcn_sched_barrier(0);                   // ... and the Z1 MFMAs issue before it
     CHAIN_STAMP(1);
     __syncthreads();
@@ -401,14 +480,14 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
       ba0 = tr_pair(rtr, rtr + 256);
       ba1 = tr_pair(rtr + 8, rtr + 264);
     }
-    // ---- output + loss of sample sl (every wave redundantly, identical results)
+    // ---- output + loss of sample ls (every wave redundantly, identical results)
     float d0, d1, d2, lr_step;
     float o_keep[3], tt_keep[3], p_keep[3];     // for the optional loss log
     {
-      const float4 a0 = *reinterpret_cast<const float4*>(&sm.po[buf][0][sl][0]);
-      const float4 a1 = *reinterpret_cast<const float4*>(&sm.po[buf][1][sl][0]);
-      const float4 a2 = *reinterpret_cast<const float4*>(&sm.po[buf][2][sl][0]);
-      const float4 a3 = *reinterpret_cast<const float4*>(&sm.po[buf][3][sl][0]);
+      const float4 a0 = *reinterpret_cast<const float4*>(&sm.po[buf][0][ls][0]);
+      const float4 a1 = *reinterpret_cast<const float4*>(&sm.po[buf][1][ls][0]);
+      const float4 a2 = *reinterpret_cast<const float4*>(&sm.po[buf][2][ls][0]);
+      const float4 a3 = *reinterpret_cast<const float4*>(&sm.po[buf][3][ls][0]);
       const float o0 = (((a0.x + a1.x) + a2.x) + a3.x) + b2_0;
       const float o1 = (((a0.y + a1.y) + a2.y) + a3.y) + b2_1;
       const float o2 = (((a0.z + a1.z) + a2.z) + a3.z) + b2_2;
@@ -477,12 +556,7 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
           acc -= (tt_keep[k] * (float)CHAIN_MB) * __logf(fminf(fmaxf(p_keep[k], 1e-7f), 1.0f - 1e-7f));
         Ls = acc;
       }
-      float x = (g & 1) == 0 ? Ls : 0.f;     // the 32 distinct samples: rows 0 and 2
-      x = x + dpp_any(x, 0x128);
-      x = x + dpp_any(x, 0x124);
-      x = x + dpp_any(x, 0x122);
-      x = x + dpp_any(x, 0x121);
-      x = sum_x32(sum_x16(x));
+      const float x = tot32(Ls);             // the 32 samples, round-3 order
       if (w == 0 && l == 0) {
         const int in_u = t % spu;
         loss_acc += x * invm;
@@ -493,68 +567,45 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
         }
       }
     }
-    sm.dm[w][0][prow] = d0;
-    sm.dm[w][1][prow] = d1;
-    sm.dm[w][2][prow] = d2;
-    float gb2[3] = {d0, d1, d2};     // sum over the 32 samples: the row's 16, then rows g ^ 2
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      float x = gb2[k];
-      x = x + dpp_any(x, 0x128);
-      x = x + dpp_any(x, 0x124);
-      x = x + dpp_any(x, 0x122);
-      x = x + dpp_any(x, 0x121);
-      gb2[k] = x;                    // the row's sum; rows g ^ 2 join in the update's swaps
-    }
+    // gb2 = the 32-sample sums of d (round-3 order): gb2[0] in every lane, gb2[1] in rows 0 / 1
+    // and gb2[2] in rows 2 / 3 (U, the rows that own b2[1] / b2[2])
+    const float G0 = tot32(d0);
+    const float U = tot32_pair(d1, d2);
     CHAIN_STAMP(3);
     // ---- backward in the sample-major layout: samples 16 mt + 4g + r, hidden 16w + c
-    float4 dA[3], dB[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      dA[k] = *reinterpret_cast<const float4*>(&sm.dm[w][k][4 * g]);
-      dB[k] = *reinterpret_cast<const float4*>(&sm.dm[w][k][16 + 4 * g]);
-    }
     if (!RELU) {
       ba0 = tr_pair(rtr, rtr + 256);
       ba1 = tr_pair(rtr + 8, rtr + 264);
     }
     float dz[8];
-    float g2_0 = 0.f, g2_1 = 0.f, g2_2 = 0.f;
+    float g2_0, g2_1, g2_2;          // started by slot 0 (bwd_dpp<0>)
+    {
+      const float zz[8] = {zs0[0], zs0[1], zs0[2], zs0[3], zs1[0], zs1[1], zs1[2], zs1[3]};
+      float dh[8];
+#define NFSP_BWD_SLOT(J) dh[J] = bwd_dpp<J>(g2_0, g2_1, g2_2, d0, d1, d2, fmaxf(zz[J], 0.f), W2_0, W2_1, W2_2)
+      NFSP_BWD_SLOT(0); NFSP_BWD_SLOT(1); NFSP_BWD_SLOT(2); NFSP_BWD_SLOT(3);
+      NFSP_BWD_SLOT(4); NFSP_BWD_SLOT(5); NFSP_BWD_SLOT(6); NFSP_BWD_SLOT(7);
+#undef NFSP_BWD_SLOT
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int r = j & 3;
-      const float z = j < 4 ? zs0[r] : zs1[r];
-      const float4 e0 = j < 4 ? dA[0] : dB[0], e1 = j < 4 ? dA[1] : dB[1], e2 = j < 4 ? dA[2] : dB[2];
-      const float x0 = r == 0 ? e0.x : r == 1 ? e0.y : r == 2 ? e0.z : e0.w;
-      const float x1 = r == 0 ? e1.x : r == 1 ? e1.y : r == 2 ? e1.z : e1.w;
-      const float x2 = r == 0 ? e2.x : r == 1 ? e2.y : r == 2 ? e2.z : e2.w;
-      const float h = fmaxf(z, 0.f);
-      g2_0 += h * x0;
-      g2_1 += h * x1;
-      g2_2 += h * x2;
-      const float dh = (x0 * W2_0 + x1 * W2_1) + x2 * W2_2;
-      dz[j] = z > 0.f ? dh : 0.f;
+      for (int j = 0; j < 8; ++j) dz[j] = zz[j] > 0.f ? dh[j] : 0.f;
     }
     bf16x8 dhi, dmid, dlo;
     split3(dz, dhi, dmid, dlo, SK);
     // dW1[16 it + 4g + r][16w + c] = sum over the 32 samples in dz's K order (row 30: gb1)
     const floatx4 gA = mfma3(ba0, dhi, dmid, dlo);
     const floatx4 gB = mfma3(ba1, dhi, dmid, dlo);
-    // The four row totals of (g2_0, g2_1, g2_2, gb2 row sums of output 0) in one transpose:
-    // two swaps across rows g ^ 2, one across g ^ 1 leave g2_0's total in row 0, g2_2's in row 1,
-    // g2_1's in row 2 and 2 gb2[0] in row 3 (rows 0 / 1 and 2 / 3 hold the same samples' sums),
-    // each added (r0 + r2) + (r1 + r3) as sum_x16(sum_x32(.)) did; gb2[1] / gb2[2] in one more
-    // swap, rows 0-1 / 2-3.  Each row updates the values it holds (own1, own2).
-    float V, U;
+    // The four row totals of (g2_0, g2_1, g2_2, gb2[0]) in one transpose: two swaps across
+    // rows g ^ 2, one across g ^ 1 leave g2_0's total in row 0, g2_2's in row 1, g2_1's in row 2
+    // and 4 gb2[0] in row 3 (gb2[0] is in every row), each added (r0 + r2) + (r1 + r3) as
+    // sum_x16(sum_x32(.)) did.  Each row updates the values it holds (own1, own2).
+    float V;
     {
       const auto ab = __builtin_amdgcn_permlane32_swap(__float_as_uint(g2_0), __float_as_uint(g2_1), false, false);
       const float tab = __uint_as_float(ab[0]) + __uint_as_float(ab[1]);
-      const auto cd = __builtin_amdgcn_permlane32_swap(__float_as_uint(g2_2), __float_as_uint(gb2[0]), false, false);
+      const auto cd = __builtin_amdgcn_permlane32_swap(__float_as_uint(g2_2), __float_as_uint(G0), false, false);
       const float tcd = __uint_as_float(cd[0]) + __uint_as_float(cd[1]);
       const auto z = __builtin_amdgcn_permlane16_swap(__float_as_uint(tab), __float_as_uint(tcd), false, false);
       V = __uint_as_float(z[0]) + __uint_as_float(z[1]);
-      const auto uu = __builtin_amdgcn_permlane32_swap(__float_as_uint(gb2[1]), __float_as_uint(gb2[2]), false, false);
-      U = __uint_as_float(uu[0]) + __uint_as_float(uu[1]);
     }
     CHAIN_STAMP(4);
     const float lr = lr_step;
@@ -568,7 +619,7 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
       wr[r] = wr[r] - lr * gA[r];
       wr[4 + r] = wr[4 + r] - lr * gB[r];
     }
-    stash(t + 2, va);
+    stash_slot(PH >= 0 ? ((PH + 2) & 3) : ((t + 2) & 3), va);
     CHAIN_STAMP(5);
   };
   if (t < T1) {
@@ -585,7 +636,19 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
     // drain the prologue's loads: the loop header then merges no pending load into the
     // registers the loop reuses (else every step waits on its fresh record load)
     __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0) (gfx9 encoding: expcnt 7, lgkmcnt 15)
-    for (; t < T1; ++t) step();
+    if (spu % 4 == 0) {    // t and T1 are multiples of 4: ring slots and po buffers are constants
+      for (; t < T1; ++t) {
+        step(std::integral_constant<int, 0>{});
+        ++t;
+        step(std::integral_constant<int, 1>{});
+        ++t;
+        step(std::integral_constant<int, 2>{});
+        ++t;
+        step(std::integral_constant<int, 3>{});
+      }
+    } else {
+      for (; t < T1; ++t) step(std::integral_constant<int, -1>{});
+    }
   }
 #ifdef NFSP_CHAIN_STAMPS
   if (l == 0) {
