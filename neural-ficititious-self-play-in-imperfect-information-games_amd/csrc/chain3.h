@@ -53,6 +53,10 @@ struct ChainArgs {
 #endif
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+// A 16-byte LDS read of which 12 bytes are used.  Through HIP's float4 the compiler narrows
+// it to ds_read_b96, which takes 8 LDS cycles per wave instead of ds_read_b128's 4
+// (MI355X_MICROARCH.md, LDS table); through the vector type it stays ds_read_b128.
+__device__ inline floatx4 lds4(const void* p) { return *reinterpret_cast<const floatx4*>(p); }
 
 __device__ inline float dpp_f(float x, int ctrl) {
   switch (ctrl) {   // the control word must be an immediate
@@ -426,13 +430,13 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
     float W2h[4][3];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float4 q = sm.w2t[w][4 * g + r];
-      W2h[r][0] = q.x; W2h[r][1] = q.y; W2h[r][2] = q.z;
+      const floatx4 q = lds4(&sm.w2t[w][4 * g + r]);
+      W2h[r][0] = q[0]; W2h[r][1] = q[1]; W2h[r][2] = q[2];
     }
-    const float4 w2c = sm.w2t[w][c];             // W2 of this lane's hidden unit (backward)
-    const float W2_0 = w2c.x, W2_1 = w2c.y, W2_2 = w2c.z;
-    const float4 b2v = *reinterpret_cast<const float4*>(&sm.b2s[w][0]);
-    const float b2_0 = b2v.x, b2_1 = b2v.y, b2_2 = b2v.z;
+    const floatx4 w2c = lds4(&sm.w2t[w][c]);     // W2 of this lane's hidden unit (backward)
+    const float W2_0 = w2c[0], W2_1 = w2c[1], W2_2 = w2c[2];
+    const floatx4 b2v = lds4(&sm.b2s[w][0]);
+    const float b2_0 = b2v[0], b2_1 = b2v[1], b2_2 = b2v[2];
     // Z1^T first (layer 2 waits on it); Z1 (needed only by the backward) is issued after
     // layer 2, so its matrix-core time overlaps the barrier wait
     const floatx4 zh0 = mfma3t(whi, wmid, wlo, fa0);     // Z1^T: hidden 16w+4g+r, sample c
@@ -484,13 +488,13 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
     float d0, d1, d2, lr_step;
     float o_keep[3], tt_keep[3], p_keep[3];     // for the optional loss log
     {
-      const float4 a0 = *reinterpret_cast<const float4*>(&sm.po[buf][0][ls][0]);
-      const float4 a1 = *reinterpret_cast<const float4*>(&sm.po[buf][1][ls][0]);
-      const float4 a2 = *reinterpret_cast<const float4*>(&sm.po[buf][2][ls][0]);
-      const float4 a3 = *reinterpret_cast<const float4*>(&sm.po[buf][3][ls][0]);
-      const float o0 = (((a0.x + a1.x) + a2.x) + a3.x) + b2_0;
-      const float o1 = (((a0.y + a1.y) + a2.y) + a3.y) + b2_1;
-      const float o2 = (((a0.z + a1.z) + a2.z) + a3.z) + b2_2;
+      const floatx4 a0 = lds4(&sm.po[buf][0][ls][0]);
+      const floatx4 a1 = lds4(&sm.po[buf][1][ls][0]);
+      const floatx4 a2 = lds4(&sm.po[buf][2][ls][0]);
+      const floatx4 a3 = lds4(&sm.po[buf][3][ls][0]);
+      const float o0 = (((a0[0] + a1[0]) + a2[0]) + a3[0]) + b2_0;
+      const float o1 = (((a0[1] + a1[1]) + a2[1]) + a3[1]) + b2_1;
+      const float o2 = (((a0[2] + a1[2]) + a2[2]) + a3[2]) + b2_2;
       lr_step = tg.w;
       const float tt[3] = {tg.x, tg.y, tg.z};
       o_keep[0] = o0; o_keep[1] = o1; o_keep[2] = o2;
