@@ -558,10 +558,10 @@ def rooflines(config, cfg, k_ms, k_launches, k_step_ms, br_upd, ar_upd, ar_max, 
 
     def chain_issue(name, updates, net):
         """The chain's step as an issue roofline: the loop's static issue cycles per SGD step
-        (tools/chain_census.py -> profiles/r03_chain_census.json, MI355X_MICROARCH.md issue
+        (tools/chain_census.py -> profiles/r04_chain_census.json, MI355X_MICROARCH.md issue
         costs) against the measured cycles per step at the chain's effective clock (2.40 GHz,
         tools/chain_clock.py).  frac = the share of the step one wave spends issuing."""
-        path = os.path.join(REPO, "profiles", "r03_chain_census.json")
+        path = os.path.join(REPO, "profiles", "r04_chain_census.json")
         n = max(k_launches[name], 1) * (par if name == "k_chain3_br" else 1)
         steps = updates * 2 * 128 / 32 / n                  # epochs x minibatches per workgroup
         if not os.path.exists(path) or steps <= 0:
@@ -571,7 +571,7 @@ def rooflines(config, cfg, k_ms, k_launches, k_step_ms, br_upd, ar_upd, ar_max, 
         measured = k_ms[name] * 1e-3 / steps * CHAIN_CLOCK_HZ
         out = {"kernel": name, "bound": "issue", "achieved": issue, "peak": measured,
                "unit": "cycles per SGD step (static issue / measured)", "frac": issue / measured,
-               "us_per_step": k_ms[name] * 1e3 / steps, "source": "profiles/r03_chain_census.json"}
+               "us_per_step": k_ms[name] * 1e3 / steps, "source": "profiles/r04_chain_census.json"}
         pmc = os.path.join(REPO, "profiles", "r03_chain_pmc.json")   # tools/chain_pmc.sh
         if os.path.exists(pmc):
             with open(pmc) as f:

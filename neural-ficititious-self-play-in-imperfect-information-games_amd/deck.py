@@ -34,9 +34,6 @@ class Card:
     def __str__(self):
         return f"{self._named_rank} {self._named_suit} {self._rank} {self._suit}"
 
-    def _print_human_style(self):
-        print(str(self._named_suit + ' ' + self._named_rank))
-
     @property
     def rank(self):
         return self._rank
@@ -46,7 +43,7 @@ class Deck:
     """Six cards, 2 suits x 3 ranks (leduc/deck.py:27-55)."""
 
     def __init__(self, size=6):
-        assert size > 0 and size % 2 == 0, 'Decksize has to be an even number which is greater than 0.'
+        assert size > 0 and size % 2 == 0, f'deck size must be a positive even number, got {size}'
         self._size = size
         self._fill()
         self.fake_pub = Card(-1, -1)
@@ -64,5 +61,6 @@ class Deck:
         return self._cards.pop()
 
     def print_deck(self):
-        for card in self._cards:
-            print(card.__str__())
+        """One line per remaining card, bottom of the deck first (leduc/deck.py:53-55)."""
+        if self._cards:
+            print("\n".join(map(str, self._cards)))

@@ -10,7 +10,7 @@ vector issue for 8 of its 16 cycles), s_nop 4; LDS / VMEM / SALU / waitcnt / bra
 bench.py divides that issue estimate by the measured cycles per step: the fraction of a
 step one wave spends issuing (the chain is one wave per SIMD, so nothing else fills it).
 
-    python tools/chain_census.py > profiles/r02_chain_census.json
+    python tools/chain_census.py > profiles/r04_chain_census.json
 """
 import collections
 import json
@@ -87,8 +87,14 @@ def main():
             k, c = price(op)
             cls[k] += n
             cyc[k] += n * c
-        out[name] = {"instructions": len(body), "by_class": dict(cls), "issue_cycles": dict(cyc),
-                     "issue_cycles_per_step": sum(cyc.values())}
+        # the loop may hold several SGD steps (k_chain3 unrolls by 4 when the steps per update
+        # are a multiple of 4): one s_barrier per step
+        steps = max(ops.get("s_barrier", 1), 1)
+        out[name] = {"instructions": len(body), "steps_per_iteration": steps,
+                     "instructions_per_step": len(body) / steps,
+                     "by_class": {k: v / steps for k, v in cls.items()},
+                     "issue_cycles": {k: v / steps for k, v in cyc.items()},
+                     "issue_cycles_per_step": sum(cyc.values()) / steps}
     print(json.dumps(out, indent=1))
 
 
