@@ -2,7 +2,8 @@
 kernel stays at or below its peak, and the rollout's HBM framing counts the lanes ONE launch
 plays (one slice: n_lanes / slices), not the whole step's.  Round 3's line divided the step's
 1M lanes' bytes by one 65,536-lane launch's duration and reported frac 2.1.
-Inputs: the event-timed pass of profiles/r03_bench_default.json (kernel_ms = ms per launch,
+Inputs: the event-timed pass of profiles/r04_bench_measure.json (this round's final chain, the
+bench line of tools/measure.sh) and round 3's lines (kernel_ms = ms per launch,
 kernel_ms_per_step = ms per step, per_step = the pass's updates and inserts)."""
 import json
 import math
@@ -12,8 +13,8 @@ import pytest
 
 from conftest import REPO
 
-PROFILES = [("r03_bench_default.json", "c3"), ("r03_c2_bench.json", "c2"), ("r03_c5_bench.json", "c5"),
-            ("r03_c5_tb_bench.json", "c5_tb")]
+PROFILES = [("r04_bench_measure.json", "c3"), ("r03_bench_default.json", "c3"), ("r03_c2_bench.json", "c2"),
+            ("r03_c5_bench.json", "c5"), ("r03_c5_tb_bench.json", "c5_tb")]
 
 
 def _inputs(d):
@@ -63,9 +64,9 @@ def test_every_frac_at_most_one(name, config):
 def test_c3_rollout_frac_reproduces_from_the_kernel_stats():
     """C3's rollout: ~1.44 KB of reference-layout tuples per hand x 65,536 lanes per launch over
     the launch's 0.09 ms = ~1.05 TB/s, frac ~0.13 -- the same figure from the rocprofv3 average
-    of the same tree's launches (profiles/r03_c3_kernel_stats.csv)."""
+    of the same tree's launches (profiles/r04_c3_kernel_stats.csv, tools/measure.sh)."""
     import bench
-    with open(os.path.join(REPO, "profiles", "r03_bench_default.json")) as f:
+    with open(os.path.join(REPO, "profiles", "r04_bench_measure.json")) as f:
         d = json.load(f)
     cfg = dict(bench.CONFIGS["c3"])
     _, other, _, _ = bench.rooflines("c3", cfg, *_inputs(d))
@@ -73,12 +74,28 @@ def test_c3_rollout_frac_reproduces_from_the_kernel_stats():
     assert 0.11 <= r["frac"] <= 0.15, r
     # the rocprof average duration of k_rollout in the committed kernel stats
     import csv
-    with open(os.path.join(REPO, "profiles", "r03_c3_kernel_stats.csv")) as f:
+    with open(os.path.join(REPO, "profiles", "r04_c3_kernel_stats.csv")) as f:
         rows = [row for row in csv.DictReader(f) if "::k_rollout(" in row["Name"]]
     assert rows
     avg_ms = float(rows[0]["AverageNs"]) * 1e-6
     frac_rocprof = r["bytes_per_hand"] * 65_536 / (avg_ms * 1e-3) / 1e9 / bench.PEAK_HBM_GBS
     assert abs(frac_rocprof - r["frac"]) <= 0.02, (frac_rocprof, r["frac"])
+
+
+def test_c3_dominant_chain_duration_agrees_with_rocprof():
+    """The headline's roofline kernel (the chain on the critical stream) has the same average
+    launch duration in bench's live HIP-event pass and in the rocprofv3 kernel statistics of the
+    same command (tools/measure.sh): within 5 %."""
+    import csv
+    with open(os.path.join(REPO, "profiles", "r04_bench_measure.json")) as f:
+        d = json.load(f)
+    roof = d["roofline"]
+    inst = {"k_chain3_ar": "k_chain3<0, 0, 0>", "k_chain3_br": "k_chain3<1, 0, 0>"}[roof["kernel"]]
+    with open(os.path.join(REPO, "profiles", "r04_c3_kernel_stats.csv")) as f:
+        rows = [row for row in csv.DictReader(f) if inst in row["Name"]]
+    assert rows
+    avg_ms = float(rows[0]["AverageNs"]) * 1e-6
+    assert abs(avg_ms - roof["avg_ms"]) <= 0.05 * avg_ms, (avg_ms, roof["avg_ms"])
 
 
 def test_cpu_share_is_bounded_by_the_machine():
