@@ -557,6 +557,11 @@ int engine_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, bool own_streams, n
                "unknown bits in quirks (NFSP_QUIRK_* | NFSP_EXT_*)");
   NFSP_REQUIRE(!(cfg->quirks & NFSP_EXT_MSE_Q) || (cfg->quirks & NFSP_EXT_LINEAR_Q),
                "NFSP_EXT_MSE_Q requires NFSP_EXT_LINEAR_Q");
+  // the chains read an agent's step records through a buffer descriptor with 32-bit offsets
+  // (k_chain3): [umax][epochs][batch / 32] records of one learner call must stay below 2 GiB
+  NFSP_REQUIRE((4 * (int64_t)(cfg->n_lanes / cfg->slices) / cfg->inserts_per_update + 2) * cfg->epochs *
+                       (cfg->batch / CHAIN_MB) * (int64_t)sizeof(StepRec) < (1ll << 31),
+               "one slice's step records exceed 2 GiB: use more slices (or more inserts per update)");
   *out = nullptr;
   nfsp_engine* e = new nfsp_engine();
   e->ctx = ctx;

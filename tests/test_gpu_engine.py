@@ -227,3 +227,13 @@ def test_engine_rejects_unknown_quirk_bits(pkg):
     eng = pkg.engine.SelfPlayEngine(n_lanes=64, quirks=pkg.native.QUIRKS_REFERENCE | pkg.native.TEXTBOOK_MSE)
     eng.step()
     assert eng.stats()["hands"] == 64
+
+
+def test_engine_rejects_step_records_past_the_chains_32_bit_offsets(pkg):
+    """k_chain3 reads an agent's step records through a buffer descriptor with 32-bit offsets:
+    a slice whose records would pass 2 GiB is refused at creation, before any allocation."""
+    with pytest.raises(pkg.native.NativeError, match="exceed 2 GiB"):
+        pkg.engine.SelfPlayEngine(n_lanes=1 << 23, inserts_per_update=32)
+    eng = pkg.engine.SelfPlayEngine(n_lanes=1 << 23, slices=8, inserts_per_update=32, rl_capacity=1000,
+                                    sl_capacity=1000)
+    eng.close()
