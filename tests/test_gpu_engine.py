@@ -234,6 +234,6 @@ def test_engine_rejects_step_records_past_the_chains_32_bit_offsets(pkg):
     a slice whose records would pass 2 GiB is refused at creation, before any allocation."""
     with pytest.raises(pkg.native.NativeError, match="exceed 2 GiB"):
         pkg.engine.SelfPlayEngine(n_lanes=1 << 23, inserts_per_update=32)
-    eng = pkg.engine.SelfPlayEngine(n_lanes=1 << 23, slices=8, inserts_per_update=32, rl_capacity=1000,
+    eng = pkg.engine.SelfPlayEngine(n_lanes=1 << 23, slices=16, inserts_per_update=32, rl_capacity=1000,
                                     sl_capacity=1000)
     eng.close()
