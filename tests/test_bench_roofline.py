@@ -82,16 +82,19 @@ def test_c3_rollout_frac_reproduces_from_the_kernel_stats():
     assert abs(frac_rocprof - r["frac"]) <= 0.02, (frac_rocprof, r["frac"])
 
 
-def test_c3_dominant_chain_duration_agrees_with_rocprof():
+@pytest.mark.parametrize("line,stats", [("r04_bench_measure.json", "r04_c3_kernel_stats.csv"),
+                                        ("r04_driver_cmd_prof_bench.json", "r04_driver_cmd_kernel_stats.csv")])
+def test_c3_dominant_chain_duration_agrees_with_rocprof(line, stats):
     """The headline's roofline kernel (the chain on the critical stream) has the same average
     launch duration in bench's live HIP-event pass and in the rocprofv3 kernel statistics of the
-    same command (tools/measure.sh): within 5 %."""
+    same command (tools/measure.sh; tools/prof_driver_cmd.sh: the driver's own command,
+    --steps 20 --warmup 5): within 5 %."""
     import csv
-    with open(os.path.join(REPO, "profiles", "r04_bench_measure.json")) as f:
+    with open(os.path.join(REPO, "profiles", line)) as f:
         d = json.load(f)
     roof = d["roofline"]
     inst = {"k_chain3_ar": "k_chain3<0, 0, 0>", "k_chain3_br": "k_chain3<1, 0, 0>"}[roof["kernel"]]
-    with open(os.path.join(REPO, "profiles", "r04_c3_kernel_stats.csv")) as f:
+    with open(os.path.join(REPO, "profiles", stats)) as f:
         rows = [row for row in csv.DictReader(f) if inst in row["Name"]]
     assert rows
     avg_ms = float(rows[0]["AverageNs"]) * 1e-6
