@@ -29,6 +29,7 @@ for v in "$@"; do
     k32_ar_g*) run $v --slices 32 --slice-lag 2 --xchg-every 1 --xchg-scale $(python3 -c "print(${v#k32_ar_g} / 8)") ;;
     k16_ar_g*) run $v --slices 16 --slice-lag 2 --xchg-every 1 --xchg-scale $(python3 -c "print(${v#k16_ar_g} / 8)") ;;
     k64_ar_g*) run $v --slices 64 --slice-lag 2 --xchg-every 1 --xchg-scale $(python3 -c "print(${v#k64_ar_g} / 8)") ;;
+    k128_ar_g*) run $v --slices 128 --slice-lag 2 --xchg-every 1 --xchg-scale $(python3 -c "print(${v#k128_ar_g} / 8)") ;;
     k32_ar_s*) run $v --slices 32 --slice-lag 2 --xchg-every 1 --xchg-scale ${v#k32_ar_s} ;;
     k64_ar_s*) run $v --slices 64 --slice-lag 2 --xchg-every 1 --xchg-scale ${v#k64_ar_s} ;;
     k64_arbr_s*) run $v --slices 64 --slice-lag 2 --xchg-every 1 --xchg-nets arbr --xchg-scale ${v#k64_arbr_s} ;;
