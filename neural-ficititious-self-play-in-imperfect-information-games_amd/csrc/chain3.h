@@ -53,10 +53,48 @@ struct ChainArgs {
 #endif
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx2 __attribute__((ext_vector_type(2)));
 // A 16-byte LDS read of which 12 bytes are used.  Through HIP's float4 the compiler narrows
 // it to ds_read_b96, which takes 8 LDS cycles per wave instead of ds_read_b128's 4
 // (MI355X_MICROARCH.md, LDS table); through the vector type it stays ds_read_b128.
 __device__ inline floatx4 lds4(const void* p) { return *reinterpret_cast<const floatx4*>(p); }
+// The same, volatile (through an LDS pointer: a generic volatile pointer becomes a flat load):
+// a read whose first two components feed packed f32 instructions is otherwise still narrowed
+// to ds_read_b96.
+typedef __attribute__((address_space(3))) const volatile floatx4 lds_vfloatx4;
+__device__ inline floatx4 lds4v(const void* p) { return *(lds_vfloatx4*)p; }
+
+// Packed f32 (v_pk_fma_f32 / v_pk_mul_f32: two values per instruction, each half rounded
+// exactly as the scalar instruction) where a step has pairs of independent scalar operations
+// (round 4, tools/ar_var.sh; weight hashes after 400 updates identical to the scalar chain):
+//   PK_W   the W1 update (8 fma -> 4), both chains
+//   PK_SM  AR softmax: y = e / S and d = y T_M - m for outputs 0 / 1
+//   PK_L2  layer 2: the two sample halves' partial outputs (24 fma -> 12)
+//   PK_O   outputs 0 / 1 of the 4-wave partial sums (8 add -> 4)
+// Kept: BR PK_W, AR PK_W | PK_SM (AR 0.788 -> 0.761 us per SGD step in the microbenchmark).
+// Not kept, because their results were not reproducible:
+//  * PK_L2 in the AR chain (whose Z1 MFMAs are scheduled freely, see the fences in the
+//    step): the weights differed on every run (4e-3 .. 9e-3 from the f32 reference chain
+//    after 200 updates); in that schedule a packed FMA overwrote the SrcC registers of a
+//    dependent MFMA 2-3 wait states after it issued;
+//  * PK_L2 / PK_O in the BR chain: bit-identical and 0.750 -> 0.712 us with a CU per chain,
+//    but with 4 chain workgroups per CU (engine groups of 200 replicas,
+//    tests/test_gpu_group.py) replicas differed from standalone engines by up to 3e-4 on
+//    some runs (tools/group_share_probe.py).  Their schedules overwrite the SrcC or result
+//    registers of in-flight MFMAs by VALU instructions 4-7 wait states after issue 16 times
+//    per step, against 4 in the scalar chain: the compiler's MFMA hazard padding is not
+//    enough there when other waves share the matrix cores.  Every kept variant was checked
+//    with that probe (R = 200, exact) as well as the GPU parity suite.
+//  * also measured: PK_O in the AR chain (0.772, slower), the BR Huber loss on pairs (0.737).
+constexpr unsigned PK_L2 = 1, PK_O = 2, PK_W = 4, PK_SM = 8;
+#ifndef NFSP_PK_AR                 // build-time override, for A/B builds (tools/build_lib_variant.py)
+#define NFSP_PK_AR (PK_W | PK_SM)
+#endif
+#ifndef NFSP_PK_BR
+#define NFSP_PK_BR (PK_W)
+#endif
+template <int RELU>
+constexpr unsigned chain_pk() { return RELU == 0 ? (NFSP_PK_AR) : (NFSP_PK_BR); }
 
 __device__ inline float dpp_f(float x, int ctrl) {
   switch (ctrl) {   // the control word must be an immediate
@@ -324,6 +362,7 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   Chain3Smem& sm = *reinterpret_cast<Chain3Smem*>(smem_raw);
   const ChainJob J = TABLE ? C.jobs[blockIdx.x] : C.job[blockIdx.x];
+  constexpr unsigned PK = chain_pk<RELU>();
   const int tid = threadIdx.x;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l = tid & 63;
@@ -430,7 +469,7 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
     float W2h[4][3];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const floatx4 q = lds4(&sm.w2t[w][4 * g + r]);
+      const floatx4 q = (PK & PK_L2) ? lds4v(&sm.w2t[w][4 * g + r]) : lds4(&sm.w2t[w][4 * g + r]);
       W2h[r][0] = q[0]; W2h[r][1] = q[1]; W2h[r][2] = q[2];
     }
     const floatx4 w2c = lds4(&sm.w2t[w][c]);     // W2 of this lane's hidden unit (backward)
@@ -445,16 +484,31 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
     CHAIN_STAMP(0);
     // ---- layer 2 partial over the slice, from Z1^T
     float p0[3], p1[3];
+    if constexpr (PK & PK_L2) {     // the two sample halves as pairs
+      floatx2 P[3];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) { p0[k] = 0.f; p1[k] = 0.f; }
+      for (int k = 0; k < 3; ++k) P[k] = floatx2{0.f, 0.f};
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float h0 = fmaxf(zh0[r], 0.f);        // b1 is W1's row 30 (CHAIN_BIAS_IN)
-      const float h1 = fmaxf(zh1[r], 0.f);
+      for (int r = 0; r < 4; ++r) {
+        const floatx2 H = {fmaxf(zh0[r], 0.f), fmaxf(zh1[r], 0.f)};
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        p0[k] = p0[k] + h0 * W2h[r][k];
-        p1[k] = p1[k] + h1 * W2h[r][k];
+        for (int k = 0; k < 3; ++k)
+          P[k] = __builtin_elementwise_fma(H, floatx2{W2h[r][k], W2h[r][k]}, P[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < 3; ++k) { p0[k] = P[k].x; p1[k] = P[k].y; }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) { p0[k] = 0.f; p1[k] = 0.f; }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float h0 = fmaxf(zh0[r], 0.f);        // b1 is W1's row 30 (CHAIN_BIAS_IN)
+        const float h1 = fmaxf(zh1[r], 0.f);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          p0[k] = p0[k] + h0 * W2h[r][k];
+          p1[k] = p1[k] + h1 * W2h[r][k];
+        }
       }
     }
     const int buf = PH >= 0 ? (PH & 1) : (t & 1);
@@ -492,12 +546,20 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
     float d0, d1, d2, lr_step;
     float o_keep[3], tt_keep[3], p_keep[3];     // for the optional loss log
     {
-      const floatx4 a0 = lds4(&sm.po[buf][0][ls][0]);
-      const floatx4 a1 = lds4(&sm.po[buf][1][ls][0]);
-      const floatx4 a2 = lds4(&sm.po[buf][2][ls][0]);
-      const floatx4 a3 = lds4(&sm.po[buf][3][ls][0]);
-      const float o0 = (((a0[0] + a1[0]) + a2[0]) + a3[0]) + b2_0;
-      const float o1 = (((a0[1] + a1[1]) + a2[1]) + a3[1]) + b2_1;
+      constexpr bool vo = PK & PK_O;
+      const floatx4 a0 = vo ? lds4v(&sm.po[buf][0][ls][0]) : lds4(&sm.po[buf][0][ls][0]);
+      const floatx4 a1 = vo ? lds4v(&sm.po[buf][1][ls][0]) : lds4(&sm.po[buf][1][ls][0]);
+      const floatx4 a2 = vo ? lds4v(&sm.po[buf][2][ls][0]) : lds4(&sm.po[buf][2][ls][0]);
+      const floatx4 a3 = vo ? lds4v(&sm.po[buf][3][ls][0]) : lds4(&sm.po[buf][3][ls][0]);
+      float o0, o1;
+      if constexpr (PK & PK_O) {
+        const floatx2 o01 = (((a0.xy + a1.xy) + a2.xy) + a3.xy) + floatx2{b2_0, b2_1};
+        o0 = o01.x;
+        o1 = o01.y;
+      } else {
+        o0 = (((a0[0] + a1[0]) + a2[0]) + a3[0]) + b2_0;
+        o1 = (((a0[1] + a1[1]) + a2[1]) + a3[1]) + b2_1;
+      }
       const float o2 = (((a0[2] + a1[2]) + a2[2]) + a3[2]) + b2_2;
       lr_step = tg.w;
       const float tt[3] = {tg.x, tg.y, tg.z};
@@ -533,7 +595,9 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
         const float e1 = __builtin_amdgcn_exp2f(__builtin_fmaf(o1, L2E, -mxl));
         const float e2 = __builtin_amdgcn_exp2f(__builtin_fmaf(o2, L2E, -mxl));
         const float rs = __builtin_amdgcn_rcpf((e0 + e1) + e2);
-        const float y0 = e0 * rs, y1 = e1 * rs, y2 = e2 * rs;
+        // outputs 0 / 1 as a pair (PK_SM): the same products, two per instruction
+        const floatx2 y01 = (PK & PK_SM) ? floatx2{e0, e1} * floatx2{rs, rs} : floatx2{e0 * rs, e1 * rs};
+        const float y0 = y01.x, y1 = y01.y, y2 = e2 * rs;
         const float eps = 1e-7f, hi = 1.0f - 1e-7f;
         const float q0 = y0, q1 = y1, q2 = y2;
         p_keep[0] = q0; p_keep[1] = q1; p_keep[2] = q2;
@@ -544,8 +608,14 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
         // AR records carry t / batch (k_ar_prep; a power-of-two scale, exact), so the 1 / batch
         // of both terms is already in m_k
         const float k = (m0 + m1) + m2;
-        d0 = y0 * k - m0;
-        d1 = y1 * k - m1;
+        if constexpr (PK & PK_SM) {
+          const floatx2 d01 = __builtin_elementwise_fma(y01, floatx2{k, k}, -floatx2{m0, m1});
+          d0 = d01.x;
+          d1 = d01.y;
+        } else {
+          d0 = y0 * k - m0;
+          d1 = y1 * k - m1;
+        }
         d2 = y2 * k - m2;
       }
     }
@@ -622,10 +692,20 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
       *own1 = v1 - (lr * own1_sc) * V;
       *own2 = v2 - lr * U;
     }
+    if constexpr (PK & PK_W) {      // W1 -= lr dW1, two rows per instruction
+      const floatx2 nl = {-lr, -lr};
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      wr[r] = wr[r] - lr * gA[r];
-      wr[4 + r] = wr[4 + r] - lr * gB[r];
+      for (int r = 0; r < 4; r += 2) {
+        const floatx2 a = __builtin_elementwise_fma(nl, floatx2{gA[r], gA[r + 1]}, floatx2{wr[r], wr[r + 1]});
+        const floatx2 b = __builtin_elementwise_fma(nl, floatx2{gB[r], gB[r + 1]}, floatx2{wr[4 + r], wr[5 + r]});
+        wr[r] = a.x; wr[r + 1] = a.y; wr[4 + r] = b.x; wr[5 + r] = b.y;
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        wr[r] = wr[r] - lr * gA[r];
+        wr[4 + r] = wr[4 + r] - lr * gB[r];
+      }
     }
     stash_slot(PH >= 0 ? ((PH + 2) & 3) : ((t + 2) & 3), va);
     CHAIN_STAMP(5);
