@@ -171,8 +171,8 @@ class AvgPolicyExchange:
         of the [2][NP] deltas at ptr (device), complete on return."""
         try:
             t = self._wrap(ptr, n, torch.float32, self._dev)
-            x = t.cpu()
             if self.dist.get_backend() == "gloo":
+                x = t.cpu()
                 self.dist.all_reduce(x)
                 t.copy_(x)
             else:
