@@ -435,6 +435,12 @@ int nfsp_group_set_timing(nfsp_group* g, int on);
  * count once each. */
 int nfsp_group_get_timings(nfsp_group* g, double* ms /*[10]*/, int64_t* launches /*[10]*/);
 int nfsp_group_rounds(nfsp_group* g, int64_t* out);   /* BR rounds of the last learner call */
+/* Diagnostic trace of the learner calls' plans (tools/c4_slice_spread.py: the lockstep cost of
+ * a per-slice exchange across C4 ranks).  on = 1 clears and starts it; every learner call then
+ * appends, per replica r and agent a, its AR and BR update counts: [call][r][a][AR, BR].
+ * nfsp_group_trace copies min(cap, size) int32 values and reports the size in *n. */
+int nfsp_group_set_trace(nfsp_group* g, int on);
+int nfsp_group_trace(nfsp_group* g, int32_t* out, int64_t cap, int64_t* n);
 
 /* ---- evaluation ----
  * Exact exploitability of two average-policy nets (packed weights, device pointers; e.g.

@@ -913,6 +913,8 @@ struct nfsp_group {
   int64_t calls = 0;             // learner calls (slices) so far
   int64_t rounds = 0;            // BR rounds of the last learner call (stats)
   int chain_lds = 0;             // LDS per chain workgroup: 4R chains on the device's CUs
+  bool trace_on = false;         // nfsp_group_set_trace: per call [R][2][AR, BR] update counts
+  std::vector<int32_t> trace;
 };
 
 namespace {
@@ -1078,6 +1080,12 @@ static int group_update(nfsp_group* g) {
   // every plan succeeded: the rollouts are consumed and the schedules advance (a failed
   // plan leaves every replica as it was -- pending, schedules untouched -- so they stay in step)
   for (int r = 0; r < R; ++r) commit_plan(g->eng[r], L[r]);
+  if (g->trace_on)
+    for (int r = 0; r < R; ++r)
+      for (int a = 0; a < 2; ++a) {
+        g->trace.push_back((int32_t)L[r].P.A[a].U);
+        g->trace.push_back((int32_t)L[r].P.A[a].U_br);
+      }
   // ---- tables: prep / final args per replica; the AR chains (2R workgroups, one launch);
   // per BR round k the targets and the chain of every (replica, agent) with a k-th segment
   std::vector<ChainJob> ar_jobs;
@@ -1293,5 +1301,20 @@ extern "C" int nfsp_group_step(nfsp_group* g) {
 extern "C" int nfsp_group_rounds(nfsp_group* g, int64_t* out) {
   NFSP_REQUIRE(g && out, "null argument");
   *out = g->rounds;
+  return NFSP_OK;
+}
+
+extern "C" int nfsp_group_set_trace(nfsp_group* g, int on) {
+  NFSP_REQUIRE(g, "null argument");
+  g->trace_on = on != 0;
+  g->trace.clear();
+  return NFSP_OK;
+}
+
+extern "C" int nfsp_group_trace(nfsp_group* g, int32_t* out, int64_t cap, int64_t* n) {
+  NFSP_REQUIRE(g && n && cap >= 0 && (out || cap == 0), "bad argument");
+  const int64_t m = (int64_t)g->trace.size();
+  for (int64_t i = 0; i < m && i < cap; ++i) out[i] = g->trace[i];
+  *n = m;
   return NFSP_OK;
 }

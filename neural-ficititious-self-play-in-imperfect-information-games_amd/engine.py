@@ -305,6 +305,18 @@ class EngineGroup:
         native.check(self.L.nfsp_group_rounds(self.h, C.byref(n)), "nfsp_group_rounds")
         return n.value
 
+    def set_trace(self, on=True):
+        """Start (and clear) / stop the learner-plan trace (nfsp_group_set_trace)."""
+        native.check(self.L.nfsp_group_set_trace(self.h, int(bool(on))), "nfsp_group_set_trace")
+
+    def trace(self) -> np.ndarray:
+        """The traced learner calls' update counts, [call][replica][agent][AR, BR]."""
+        n = native.I64()
+        native.check(self.L.nfsp_group_trace(self.h, None, 0, C.byref(n)), "nfsp_group_trace")
+        buf = (native.I32 * max(n.value, 1))()
+        native.check(self.L.nfsp_group_trace(self.h, buf, n.value, C.byref(n)), "nfsp_group_trace")
+        return np.frombuffer(buf, np.int32, count=n.value).reshape(-1, self.R, 2, 2).copy()
+
     def stats(self) -> dict:
         """Per-replica stats summed (counters) and listed (``replicas``)."""
         per = [e.stats() for e in self.replicas]

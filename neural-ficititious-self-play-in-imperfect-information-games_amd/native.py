@@ -120,6 +120,8 @@ SIGNATURES = {
     "nfsp_group_set_timing": (I32, [P, I32]),
     "nfsp_group_get_timings": (I32, [P, C.POINTER(F64), C.POINTER(I64)]),
     "nfsp_group_rounds": (I32, [P, C.POINTER(I64)]),
+    "nfsp_group_set_trace": (I32, [P, I32]),
+    "nfsp_group_trace": (I32, [P, C.POINTER(I32), I64, C.POINTER(I64)]),
     "nfsp_group_set_exchange": (I32, [P, U32, I32, F32]),
     "nfsp_engine_set_exchange": (I32, [P, I32, F32, P, P, P]),
     "nfsp_engine_exchanges": (I32, [P, C.POINTER(I64)]),

@@ -169,3 +169,25 @@ def test_group_replica_count_bounds(pkg):
         pkg.engine.EngineGroup(0, **SMALL)
     with pytest.raises(pkg.native.NativeError, match="replicas"):
         pkg.engine.EngineGroup(pkg.native.GROUP_MAX_REPLICAS + 1, **SMALL)
+
+
+def test_group_trace_records_every_slice_plan(pkg):
+    """nfsp_group_set_trace / nfsp_group_trace (tools/c4_slice_spread.py): one [R][agent][AR, BR]
+    row of update counts per learner call (slice), summing over the step's slices to the
+    replicas' update counters."""
+    kw = dict(n_lanes=1024, slices=4, rl_capacity=3000, sl_capacity=2000, target_every=11)
+    g = pkg.engine.EngineGroup(2, seed=77, init_seed=5, **kw)
+    g.step()
+    before = [r.stats() for r in g.replicas]
+    g.set_trace(True)
+    g.step()
+    t = g.trace()
+    g.set_trace(False)
+    after = [r.stats() for r in g.replicas]
+    assert t.shape == (4, 2, 2, 2)
+    assert g.trace().shape[0] == 0                 # stopping clears it
+    for r in range(2):
+        for a in range(2):
+            assert t[:, r, a, 1].sum() == after[r]["br_updates"][a] - before[r]["br_updates"][a]
+            assert t[:, r, a, 0].sum() >= after[r]["ar_updates"][a] - before[r]["ar_updates"][a]
+    g.close()
