@@ -76,14 +76,15 @@ CONFIGS = {
                label="C3: 1,048,576 Leduc lanes/GPU (advanced in 16 pipelined slices of 65,536), device "
                      "M_RL 200k + M_SL 2M, target sync 150, reference update cadence (1 update_strategy "
                      "/ 128 RL inserts / agent)"),
-    # C4 (BASELINE configs[3]): per GPU C3's 1M lanes and memories, as 64 pipelined slices of
-    # 16,384, and the ranks' AR nets exchanged after every slice (W0 + 2 x the mean of the
+    # C4 (BASELINE configs[3]): per GPU C3's 1M lanes and memories, as 128 pipelined slices of
+    # 8,192, and the ranks' AR nets exchanged after every slice (W0 + 2 x the mean of the
     # deltas, shards.AvgPolicyExchange, RCCL on the AR chain stream): the 8-GPU job then learns
-    # inside the CPU reference's band per total hand from its first 8.4M hands
-    # (tests/test_gpu_slices.py).  bench.py --gpus N > 1 runs it by default.
-    "c4": dict(n_lanes=1_048_576, slices=64, slice_lag=2, rl_capacity=200_000, sl_capacity=2_000_000,
+    # inside the CPU reference's band per total hand from its first 8.4M hands, >= 0.1 chips
+    # inside the bar at every checkpoint (tests/test_gpu_slices.py; 64 slices
+    # passed the first checkpoint by 0.012).  bench.py --gpus N > 1 runs it by default.
+    "c4": dict(n_lanes=1_048_576, slices=128, slice_lag=2, rl_capacity=200_000, sl_capacity=2_000_000,
                xchg_every=1, xchg_gain=2.0,
-               label="C4: 1,048,576 Leduc lanes/GPU (64 pipelined slices of 16,384), device M_RL 200k + M_SL "
+               label="C4: 1,048,576 Leduc lanes/GPU (128 pipelined slices of 8,192), device M_RL 200k + M_SL "
                      "2M, target sync 150, reference cadence; the AR nets of all GPUs exchanged after every "
                      "slice (W0 + 2 x mean of the ranks' deltas, RCCL on the AR chain stream)"),
     "c3_1slice": dict(n_lanes=1_048_576, rl_capacity=200_000, sl_capacity=2_000_000,
@@ -431,6 +432,40 @@ def rank_report(dist, backend: str, mine: dict) -> dict:
             "distinct_devices": len({(r.get("host"), r.get("pci_bus_id")) for r in ranks}) == len(ranks)}
 
 
+def refuse_host_fallback(args, world: int, fallback):
+    """Under RCCL at N > 1 the exchange must run on RCCL: a host-transport fallback (some rank
+    could not build the communicator) would time a different, slower job.  Every rank sees the
+    same fallback (AvgPolicyExchange agrees on it), so every rank exits 2 together, unless
+    --allow-host-fallback says the fallback is wanted."""
+    if fallback and args.dist_backend == "nccl" and world > 1 and not args.allow_host_fallback:
+        sys.stderr.write(f"bench.py: the AR exchange fell back to the host transport ({fallback}); "
+                         f"refusing to time it (--allow-host-fallback to accept)\n")
+        sys.exit(2)
+
+
+def check_ar_nets(dist, digest: str, when: str) -> dict:
+    """Every rank's AR-net digest (shards.ar_nets_digest); the exchange keeps the shards' AR nets
+    one net, so unequal digests mean it did not work: exit 2 on every rank."""
+    got = [None] * dist.get_world_size()
+    dist.all_gather_object(got, digest)
+    same = len(set(got)) == 1
+    if not same:
+        sys.stderr.write(f"bench.py: AR nets differ over the ranks {when}: {[g[:12] for g in got]}\n")
+        sys.exit(2)
+    return {"ar_nets_identical": True, "digest": got[0][:16]}
+
+
+def check_exchange_calls(calls: int, steps: int, slices: int, every: int) -> dict:
+    """The exchanges the timed pass made against its cadence: one per `every` learner calls,
+    one learner call per slice.  A shortfall means some slice's exchange did not run: exit 2."""
+    expected = steps * slices // every if slices % every == 0 else None
+    if expected is not None and calls != expected:
+        sys.stderr.write(f"bench.py: {calls} exchanges in the timed pass, {expected} expected "
+                         f"({steps} steps x {slices} slices / every {every})\n")
+        sys.exit(2)
+    return {"calls_timed_pass": calls, "calls_expected": expected, "calls_ok": expected is not None}
+
+
 def stub_main(args, world, rank, dist):
     """Test hook (`--stub-step-ms`): the launcher and the timing protocol with a CPU sleep in
     place of the engine step (no GPU).  Never a measurement: `data` says "stub"."""
@@ -441,18 +476,63 @@ def stub_main(args, world, rank, dist):
             sys.stderr.write(f"stub: rank {rank} fails with {fc}\n")
             os._exit(fc)
     tl = {}
-    elapsed = timed_steps(lambda: time.sleep(args.stub_step_ms * 1e-3 * (1 + 0.5 * rank)),
-                          args.steps, args.warmup, dist, device="cpu", out=tl)
+    # the exchange's protocol with a CPU stand-in: a 2 x 2,179 f32 "AR net" per rank, equal at
+    # the start, W0 + mean of the ranks' random deltas after every one of the config's slices
+    # (gloo all-reduce); --stub-rccl-fail R: rank R reports no RCCL (every rank falls back);
+    # --stub-diverge R: rank R's net is perturbed after the timed pass (the digest check fires)
+    import hashlib
+    import torch
+    slices = CONFIGS[args.config].get("slices", 1)
+    xchg = dist is not None and world > 1
+    net = torch.zeros(2 * 2179, dtype=torch.float32)
+    calls = [0]
+    fallback = None
+    if xchg:
+        ready = torch.tensor([0 if args.stub_rccl_fail is not None and rank == args.stub_rccl_fail else 1],
+                             dtype=torch.int32)
+        dist.all_reduce(ready, op=dist.ReduceOp.MIN)
+        if int(ready.item()) == 0:
+            fallback = "rccl setup failed on some rank: stub"
+        refuse_host_fallback(args, world, fallback)
+    gen = torch.Generator().manual_seed(rank)
+
+    def step():
+        for _ in range(slices):
+            if xchg:
+                d = torch.rand(net.numel(), generator=gen) * 1e-3
+                dist.all_reduce(d)
+                net.add_(d, alpha=1.0 / world)
+                calls[0] += 1
+        time.sleep(args.stub_step_ms * 1e-3 * (1 + 0.5 * rank))
+
+    def digest():
+        return hashlib.sha256(net.numpy().tobytes()).hexdigest()
+    for _ in range(args.warmup):
+        step()
+    xcheck = {}
+    if xchg:
+        xcheck["after_warmup"] = check_ar_nets(dist, digest(), "after the warmup")
+    c0 = calls[0]
+    elapsed = timed_steps(step, args.steps, 0, dist, device="cpu", out=tl)
+    c1 = calls[0]
+    if xchg and args.stub_diverge is not None and rank == args.stub_diverge:
+        net[0] += 1.0
     out = {"metric": "Leduc self-play hands/sec", "unit": "hands/s",
            "value": job_value(args.steps * lanes, world, elapsed), "n_gpus": world,
            "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": elapsed / args.steps * 1e3, "data": "stub",
            "config": {"parallelism": f"dp{world}"}}
+    if xchg:
+        xcheck["after_timed_pass"] = check_ar_nets(dist, digest(), "after the timed pass")
+        out["ar_allreduce"] = dict(check_exchange_calls(c1 - c0, args.steps, slices, 1), calls=calls[0],
+                                   transport="stub", fallback=fallback, ar_nets_check=xcheck)
     if dist is not None:
         import socket
         out["ranks"] = rank_report(dist, "gloo", dict(
             device_identity(), host=socket.gethostname(), ms_per_step=tl["local_s"] / args.steps * 1e3,
-            exchange_ms_per_call=None, exchanges=0))
+            exchange_ms_per_call=None, exchanges=c1 - c0))
+        if xchg:
+            out["ranks"]["ar_nets_identical"] = True
     if rank == 0:
         emit_result(out)
     if dist is not None:
@@ -635,7 +715,12 @@ def main():
     ap.add_argument("--xchg-transport", default="auto", choices=["auto", "rccl", "host"],
                     help="rccl: libnfsp's own communicator on the AR chain stream; host: the process "
                          "group from a host callback; auto: rccl under nccl, host under gloo")
+    ap.add_argument("--allow-host-fallback", action="store_true",
+                    help="under --dist-backend nccl at N > 1, time the job even if the AR exchange fell "
+                         "back to the host transport (default: exit 2)")
     ap.add_argument("--stub-step-ms", type=float, default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--stub-rccl-fail", type=int, default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--stub-diverge", type=int, default=None, help=argparse.SUPPRESS)
     # test hook with --stub-step-ms: rank R exits with code C after the process group is up
     ap.add_argument("--stub-fail", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--slices", type=int, default=None, help="override the config's lane slices")
@@ -692,6 +777,7 @@ def main():
         # `xchg_every`-th slice, on the AR chain stream
         avg = pkg.shards.AvgPolicyExchange(eng, dist, every=args.xchg_every, transport=args.xchg_transport,
                                            gain=args.xchg_gain)
+        refuse_host_fallback(args, world, avg.fallback)
 
     def step():
         eng.step()
@@ -699,6 +785,9 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    xcheck = {}
+    if avg is not None and world > 1:       # the exchange kept the shards' AR nets one net
+        xcheck["after_warmup"] = check_ar_nets(dist, pkg.shards.ar_nets_digest(eng), "after the warmup")
     # `value`: K steps with no instrumentation at all
     s0 = eng.stats()
     tl = {}
@@ -706,6 +795,10 @@ def main():
     elapsed = timed_steps(step, args.steps, 0, dist, torch.cuda.synchronize, device=dev, out=tl)
     x1 = avg.calls if avg is not None else 0
     s1 = eng.stats()
+    if avg is not None and world > 1:
+        xcheck["after_timed_pass"] = check_ar_nets(dist, pkg.shards.ar_nets_digest(eng), "after the timed pass")
+    xcalls = check_exchange_calls(x1 - x0, args.steps, cfg.get("slices", 1), args.xchg_every) \
+        if avg is not None else None
     # per-kernel durations: K more steps with HIP events around every launch (kernel_ms,
     # roofline); their wall time is reported beside `value`, never as it
     eng.set_timing(True)
@@ -771,7 +864,8 @@ def main():
     }
     xchg_ms = k_ms.get("ar_exchange") if avg is not None and k_launches.get("ar_exchange") else None
     if avg is not None:
-        out["ar_allreduce"] = {"calls": avg.calls, "calls_timed_pass": x1 - x0, "bytes_per_call": avg.bytes_per_call,
+        out["ar_allreduce"] = {**xcalls, "calls": avg.calls, "bytes_per_call": avg.bytes_per_call,
+                               "ar_nets_check": xcheck or None,
                                "backend": args.dist_backend, "transport": avg.transport, "fallback": avg.fallback,
                                "every_slices": args.xchg_every, "gain": args.xchg_gain,
                                "ms_per_call_event_timed": xchg_ms,
@@ -783,6 +877,8 @@ def main():
             device_identity(), host=socket.gethostname(), ms_per_step=tl["local_s"] / args.steps * 1e3,
             ms_per_step_event_timed=elapsed_ev / args.steps * 1e3,
             exchange_ms_per_call=xchg_ms, exchanges=(x1 - x0)))
+        if xcheck:
+            out["ranks"]["ar_nets_identical"] = True      # else check_ar_nets exited 2
     # exact exploitability of the AR nets after the timed steps (outside the timed region)
     ex = {m: eng.exploitability(m) for m in (0, 1)}
     out["exploitability_exact"] = {

@@ -334,7 +334,9 @@ int nfsp_engine_set_timing(nfsp_engine* e, int on);
  * nfsp_engine_update's updates and [.. + 1] = its last update's final-epoch loss (NaN: none). */
 int nfsp_engine_set_loss_log(nfsp_engine* e, int on);
 int nfsp_engine_losses(nfsp_engine* e, double* out /*[2][2][2]*/);
-int nfsp_engine_get_timings(nfsp_engine* e, double* ms /*[11]*/, int64_t* launches /*[11]*/);
+#define NFSP_TIMING_SLOTS 11
+int nfsp_engine_get_timings(nfsp_engine* e, double* ms /*[NFSP_TIMING_SLOTS]*/,
+                            int64_t* launches /*[NFSP_TIMING_SLOTS]*/);
 /* Debug view of the last learner run: per agent and role (0 = AR, 1 = BR) the sampled
  * rows [batch] (int64) and fit permutations [epochs][batch] (int32) of its LAST update. */
 int nfsp_engine_last_update(nfsp_engine* e, int agent, int role, int64_t** dev_rows,
@@ -382,7 +384,11 @@ int nfsp_engine_set_exchange(nfsp_engine* e, int every, float scale, void* rccl_
 int nfsp_engine_exchanges(nfsp_engine* e, int64_t* out);
 /* RCCL (librccl.so.1, loaded on first use): ncclGetUniqueId into out[128] (rank 0), and a
  * communicator of `world` ranks on HIP device `device` from that id (every rank, collectively:
- * ncclCommInitRank blocks until all ranks joined). */
+ * ncclCommInitRank blocks until all ranks joined).  nfsp_rccl_ready loads RCCL and selects
+ * `device` without joining anything: every rank calls it and the ranks agree (an all-reduce
+ * MIN of the results) BEFORE any of them calls nfsp_rccl_comm_create, so a rank that cannot
+ * use RCCL never leaves the others blocked in ncclCommInitRank. */
+int nfsp_rccl_ready(int device);
 int nfsp_rccl_unique_id(uint8_t* out /*[128]*/);
 int nfsp_rccl_comm_create(const uint8_t* id /*[128]*/, int world, int rank, int device, void** comm);
 int nfsp_rccl_comm_destroy(void* comm);
@@ -433,7 +439,8 @@ int nfsp_group_set_exchange(nfsp_group* g, unsigned nets, int every, float scale
 int nfsp_group_set_timing(nfsp_group* g, int on);
 /* nfsp_engine_get_timings summed over the replicas.  The shared chain and target launches
  * count once each. */
-int nfsp_group_get_timings(nfsp_group* g, double* ms /*[10]*/, int64_t* launches /*[10]*/);
+int nfsp_group_get_timings(nfsp_group* g, double* ms /*[NFSP_TIMING_SLOTS]*/,
+                           int64_t* launches /*[NFSP_TIMING_SLOTS]*/);
 int nfsp_group_rounds(nfsp_group* g, int64_t* out);   /* BR rounds of the last learner call */
 /* Diagnostic trace of the learner calls' plans (tools/c4_slice_spread.py: the lockstep cost of
  * a per-slice exchange across C4 ranks).  on = 1 clears and starts it; every learner call then

@@ -362,7 +362,10 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   Chain3Smem& sm = *reinterpret_cast<Chain3Smem*>(smem_raw);
   const ChainJob J = TABLE ? C.jobs[blockIdx.x] : C.job[blockIdx.x];
-  constexpr unsigned PK = chain_pk<RELU>();
+  // the loss-log build (a diagnostic, tests/test_gpu_nn / observability) runs the scalar forms:
+  // its extra loss code put packed writes near MFMA registers (tools/mfma_hazards.py rule 2);
+  // the packed forms round exactly as the scalar ones, so its weights are the same either way
+  constexpr unsigned PK = LOSS ? 0u : chain_pk<RELU>();
   const int tid = threadIdx.x;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l = tid & 63;

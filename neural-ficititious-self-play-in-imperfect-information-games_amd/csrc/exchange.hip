@@ -157,6 +157,16 @@ extern "C" int nfsp_engine_exchanges(nfsp_engine* e, int64_t* out) {
   return NFSP_OK;
 }
 
+extern "C" int nfsp_rccl_ready(int device) {
+  int rc = rccl_load();
+  if (rc != NFSP_OK) return rc;
+  int n = 0;
+  NFSP_HIP(hipGetDeviceCount(&n));
+  NFSP_REQUIRE(device >= 0 && device < n, "no such HIP device");
+  NFSP_HIP(hipSetDevice(device));
+  return NFSP_OK;
+}
+
 extern "C" int nfsp_rccl_unique_id(uint8_t* out) {
   NFSP_REQUIRE(out, "null argument");
   int rc = rccl_load();

@@ -125,6 +125,7 @@ SIGNATURES = {
     "nfsp_group_set_exchange": (I32, [P, U32, I32, F32]),
     "nfsp_engine_set_exchange": (I32, [P, I32, F32, P, P, P]),
     "nfsp_engine_exchanges": (I32, [P, C.POINTER(I64)]),
+    "nfsp_rccl_ready": (I32, [I32]),
     "nfsp_rccl_unique_id": (I32, [P]),
     "nfsp_rccl_comm_create": (I32, [P, I32, I32, I32, C.POINTER(P)]),
     "nfsp_rccl_comm_destroy": (I32, [P]),

@@ -43,6 +43,18 @@ from typing import Callable, Sequence
 import torch
 
 
+def ar_nets_digest(engine) -> str:
+    """sha256 of both agents' AR nets as they are now (synchronises the device): equal on
+    every rank after an exchange that worked (bench.py checks it over the ranks)."""
+    import hashlib
+    from .engine import NET_AR
+    torch.cuda.synchronize()
+    h = hashlib.sha256()
+    for a in (0, 1):
+        h.update(engine.get_weights(a, NET_AR).tobytes())
+    return h.hexdigest()
+
+
 class AvgPolicyAllReduce:
     def __init__(self, tensors: Sequence[torch.Tensor], dist, src: int = 0,
                  sync: Callable[[], None] = lambda: None):
@@ -133,22 +145,34 @@ class AvgPolicyExchange:
         L = engine.L
         self.fallback = None
         if self.transport == "rccl":
-            # rank 0's id to every rank; each rank reports whether its RCCL setup worked, and
-            # unless all did, every rank falls back to the host transport together (a job
-            # that cannot build the communicator still runs, its exchange host-synchronised)
-            uid = (C.c_uint8 * 128)()
-            ok = 1
-            if self.rank == src:
-                ok = int(L.nfsp_rccl_unique_id(uid) == native.OK)
+            # 1. every rank loads RCCL and selects its device (nfsp_rccl_ready) and the ranks
+            #    agree on the result (MIN) BEFORE anyone calls ncclCommInitRank, which blocks
+            #    until all ranks joined: a rank that cannot use RCCL never strands the others;
+            # 2. rank 0's id to every rank; 3. the communicator, its success agreed the same way.
+            # Unless every step worked on every rank, all ranks take the host transport
+            # together and `fallback` says why (bench.py refuses that under RCCL at N > 1
+            # unless --allow-host-fallback).
             dev = "cuda" if backend == "nccl" else "cpu"
-            t = torch.tensor(list(uid) + [ok], dtype=torch.uint8, device=dev)
-            dist.broadcast(t, src=src)
-            vals = t.cpu().tolist()
-            uid = (C.c_uint8 * 128)(*vals[:128])
-            comm = native.P()
+            why = ""
+            ready = int(L.nfsp_rccl_ready(torch.cuda.current_device()) == native.OK)
+            uid = (C.c_uint8 * 128)()
+            if ready and self.rank == src:
+                ready = int(L.nfsp_rccl_unique_id(uid) == native.OK)
+            if not ready:
+                why = L.nfsp_last_error().decode()
+            flag = torch.tensor([ready], dtype=torch.int32, device=dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
             rc = native.EINVAL
-            if vals[128]:
+            comm = native.P()
+            if int(flag.item()) == 1:
+                t = torch.tensor(list(uid), dtype=torch.uint8, device=dev)
+                dist.broadcast(t, src=src)
+                uid = (C.c_uint8 * 128)(*t.cpu().tolist())
                 rc = L.nfsp_rccl_comm_create(uid, self.world, self.rank, torch.cuda.current_device(), C.byref(comm))
+                if rc != native.OK:
+                    why = L.nfsp_last_error().decode()
+            elif ready:
+                why = "another rank could not load RCCL or select its device"
             good = torch.tensor([1 if rc == native.OK else 0], dtype=torch.int32, device=dev)
             dist.all_reduce(good, op=dist.ReduceOp.MIN)
             if int(good.item()) == 1:
@@ -157,7 +181,7 @@ class AvgPolicyExchange:
             else:
                 if rc == native.OK:
                     L.nfsp_rccl_comm_destroy(comm)
-                self.fallback = "rccl setup failed on some rank: " + L.nfsp_last_error().decode()
+                self.fallback = "rccl setup failed on some rank: " + (why or "another rank failed")
                 print(f"AvgPolicyExchange: {self.fallback}; using the host transport", file=sys.stderr)
                 self.transport = "host"
         if self.transport == "host":

@@ -123,3 +123,40 @@ def test_two_rank_timing_protocol():
     assert e0 == e1                           # every rank sees the max over ranks
     assert e0 >= 4 * 0.04                     # ... which is the slow rank's time
     assert v0 == v1 == 800 / e0               # whole-job units / max time
+
+
+def test_n2_line_proves_its_exchange():
+    """N > 1 with the exchange on (the stub's CPU stand-in of the AR nets, exchanged after every
+    slice over gloo): the line carries the exchanges the timed pass made against its cadence and
+    the ranks' AR-net digests, equal after the warmup and after the timed pass."""
+    rc, lines, err = _bench(["--gpus", "2", "--steps", "3", "--warmup", "1", "--stub-step-ms", "5",
+                             "--config", "c2"])
+    assert rc == 0, err
+    x = lines[0]["ar_allreduce"]
+    assert x["calls_timed_pass"] == x["calls_expected"] == 3 * 16 and x["calls_ok"]
+    assert x["fallback"] is None
+    chk = x["ar_nets_check"]
+    assert chk["after_warmup"]["ar_nets_identical"] and chk["after_timed_pass"]["ar_nets_identical"]
+    assert lines[0]["ranks"]["ar_nets_identical"] is True
+
+
+def test_host_fallback_refused_under_rccl():
+    """A rank that cannot set up RCCL makes every rank fall back to the host transport; under
+    --dist-backend nccl at N > 1 the job then exits 2 instead of timing the slower job ..."""
+    rc, lines, err = _bench(["--gpus", "2", "--steps", "2", "--warmup", "0", "--stub-step-ms", "2",
+                             "--config", "c2", "--stub-rccl-fail", "1"])
+    assert rc == 2 and not lines, err
+    assert "refusing to time it" in err
+    # ... unless the fallback is asked for; the line then says so
+    rc, lines, err = _bench(["--gpus", "2", "--steps", "2", "--warmup", "0", "--stub-step-ms", "2",
+                             "--config", "c2", "--stub-rccl-fail", "1", "--allow-host-fallback"])
+    assert rc == 0, err
+    assert lines[0]["ar_allreduce"]["fallback"].startswith("rccl setup failed")
+
+
+def test_diverged_ar_nets_end_the_job():
+    """Ranks whose AR nets differ after the timed pass (rank 1's perturbed) exit 2: no line."""
+    rc, lines, err = _bench(["--gpus", "2", "--steps", "2", "--warmup", "1", "--stub-step-ms", "2",
+                             "--config", "c2", "--stub-diverge", "1"])
+    assert rc == 2 and not lines, err
+    assert "AR nets differ over the ranks after the timed pass" in err

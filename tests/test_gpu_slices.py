@@ -249,21 +249,22 @@ def test_c3_sliced_learns_within_the_cpu_seed_band(pkg):
 
 def test_c4_emulated_learns_within_the_cpu_seed_band(pkg):
     """C4's arithmetic on one GPU, as bench.py --gpus 8 runs it (bench.CONFIGS["c4"]): 8 shards of
-    1,048,576 lanes (C3's memories each) in 64 pipelined slices (slice_lag 2), the average-policy
+    1,048,576 lanes (C3's memories each) in 128 pipelined slices (slice_lag 2), the average-policy
     nets exchanged after EVERY slice -- W0 + 2 x the mean of the shards' deltas, the rank path's
     arithmetic (tests/test_gpu_exchange.py shows the ranks equal to a group bit for bit) -- done on
     device by an engine group.  Exploitability at equal TOTAL hands against the CPU band, from the
     first checkpoint (one step = 8.4M hands) to 8 steps (67M), with the C3 bar:
     |GPU mean - CPU mean| <= 2 sigma and GPU mean <= CPU mean + 1 sigma (8 seeds each side).
-    Measured (profiles/r04_exploit_c4_slice_exchange.json): 1.526 +- 0.156 at 8.4M (the bar 1.538),
-    1.355 at 16.8M, 1.238, 1.155 at 33.5M, 1.12 at 67M, no frozen learner to 100M; round 3's
-    once-per-step exchange: 1.93 at 8.4M, in the band only from 33.5M."""
+    Besides the bar, a margin: the GPU mean sits >= 0.1 chips below CPU mean + 1 sigma at every
+    checkpoint.  Measured at 128 slices (profiles/r04_c4x_k128_ar_g2.json): 1.421 at 8.4M (bar
+    1.539), 1.234 / 1.216 / 1.165 at 16.8 / 25.2 / 33.5M; 64 slices (round 4's C4) passed 8.4M by
+    0.012 chips, round 3's once-per-step exchange reached the band only from 33.5M."""
     import bench
     c4 = bench.CONFIGS["c4"]
     band = _band()
     cpu = {int(h): np.array(v) for h, v in band["curves_by_hands"].items()}
     R, lanes, K = 8, c4["n_lanes"], c4["slices"]
-    assert (K, c4["slice_lag"], c4["xchg_every"], c4["xchg_gain"]) == (64, 2, 1, 2.0)
+    assert (K, c4["slice_lag"], c4["xchg_every"], c4["xchg_gain"]) == (128, 2, 1, 2.0)
     checkpoints = (1, 2, 3, 4, 8)                  # steps of 8 x 1,048,576 hands
     gpu = {c: [] for c in checkpoints}
     for s in range(8):
@@ -293,7 +294,7 @@ def test_c4_emulated_learns_within_the_cpu_seed_band(pkg):
     print("hands, cpu checkpoint, cpu mean, cpu std, gpu mean, gpu std:", report)
     for (h, near, cm, cs, gm, gs) in report:
         assert abs(gm - cm) <= 2 * cs, report
-        assert gm <= cm + cs, report
+        assert gm <= cm + cs - 0.1, report          # >= 0.1 chips inside the bar
 
 
 def test_pipelined_step_equals_its_declared_schedule(pkg):
