@@ -167,16 +167,18 @@ def cpu_share() -> int:
     return n
 
 
-def cpu_worker(kind: str, seconds: float, config: str, seed: int) -> dict:
+def cpu_worker(kind: str, seconds: float, config: str, seed: int, workload: str = "c") -> dict:
     """One CPU-baseline process (bench.py --cpu-worker): one replica of main.train restated
-    in C++ (kind "port") or numpy ("numpy") for `seconds`; never touches a GPU."""
+    in C++ (kind "port") or numpy ("numpy") for `seconds`; never touches a GPU.  workload
+    (BASELINE.md): "c" end to end with updates, "a" env + scheduler with random action vectors,
+    "b" the agents' play (forwards, memory inserts) without updates."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     cfg = CONFIGS[config]
     game = cfg.get("game", "leduc")
     if kind == "port":
         import cpu_port
         c = cpu_port.make_cfg(None, seed, True, game, rl_capacity=cfg["rl_capacity"],
-                              sl_capacity=cfg["sl_capacity"])
+                              sl_capacity=cfg["sl_capacity"], workload=workload)
         c.seed = c.seed + seed
         hands, el = cpu_port.bench(c, 1, seconds)
         return {"hands": int(hands), "seconds": el}
@@ -186,6 +188,11 @@ def cpu_worker(kind: str, seconds: float, config: str, seed: int) -> dict:
     env, p1, p2 = orc.make_main(init_seed=seed)
     env.kuhn = game == "kuhn"
     players = [p1, p2]
+    if workload == "a":
+        players = [orc.RandomPlayer(env), orc.RandomPlayer(env)]
+    elif workload == "b":
+        for p in players:
+            p.update_strategy = lambda: None
     dealer = random.randint(0, 1)
     hands = 0
     t0 = time.perf_counter()
@@ -197,12 +204,12 @@ def cpu_worker(kind: str, seconds: float, config: str, seed: int) -> dict:
     return {"hands": hands, "seconds": time.perf_counter() - t0}
 
 
-def cpu_processes(kind: str, procs: int, seconds: float, config: str) -> dict:
+def cpu_processes(kind: str, procs: int, seconds: float, config: str, workload: str = "c") -> dict:
     """`procs` concurrent worker processes (one per core), each an independent replica; the
     aggregate hands/s = sum of each one's hands / its own time.  Child processes, started
     fresh (no fork of a process that holds the GPU)."""
     cmd = [sys.executable, os.path.abspath(__file__), "--cpu-worker", kind, "--cpu-seconds", str(seconds),
-           "--config", config]
+           "--config", config, "--cpu-workload", workload]
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
     env.update(OMP_NUM_THREADS="1", OPENBLAS_NUM_THREADS="1", MKL_NUM_THREADS="1", HIP_VISIBLE_DEVICES="")
     ps = [subprocess.Popen(cmd + ["--cpu-seed", str(r)], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
@@ -253,6 +260,28 @@ def cpu_baseline_numpy(seconds: float, cfg_name: str, cores: int | None = None):
             "sample": f"{r['hands']} hands of main.train restated in numpy (oracle/nfsp_oracle.py: Env, "
                       f"Agent play/updates at the reference cadence, numpy fp32 MLPs) by {cores} processes "
                       f"(one per core; os.cpu_count() = {os.cpu_count()}), {seconds:.0f} s each"}
+
+
+def cpu_baseline_rollout(seconds: float, cfg_name: str, cores: int | None = None) -> dict:
+    """BASELINE.md's CPU workloads (a) and (b) -- the CPU counterparts of the line's
+    rollout_only_hands_per_s (the fused rollout + inserts, no learner): (a) main.train's env and
+    D/L/D scheduler with uniform-random action vectors; (b) the agents' play with the MLP forwards
+    (eta 0.1, eps 0.06) and the memory inserts, no updates.  Both restatements (C++ port and
+    numpy), one process per core of the job's CPU share, `seconds` each."""
+    cores = cores or cpu_share()
+    out = {"cores": cores, "os_cpu_count": os.cpu_count(), "unit": "hands/s",
+           "gpu_counterpart": "rollout_only_hands_per_s (k_rollout + k_scan + k_commit per hand)"}
+    for wl, what in (("a", "env + scheduler, uniform-random action vectors"),
+                     ("b", "Agent.play: MLP forwards + memory inserts, no updates")):
+        row = {"what": what}
+        for kind in ("port", "numpy"):
+            r = cpu_processes(kind, cores, seconds, cfg_name, wl)
+            row[kind] = {"value": r["value"], "hands": r["hands"], "per_core": sum(r["per_process"]) / cores}
+        out[wl] = row
+    out["sample"] = (f"{cores} processes x {seconds:.0f} s per workload and restatement "
+                     f"(oracle/nfsp_cpu.cpp workload 1 / 2, oracle/nfsp_oracle.py RandomPlayer / play "
+                     f"without update_strategy), config {cfg_name}")
+    return out
 
 
 def init_dist(backend=None, force: bool = False):
@@ -700,6 +729,7 @@ def main():
                     help="processes for the CPU baselines (default: this job's CPU share, cpu_share())")
     ap.add_argument("--cpu-worker", choices=["port", "numpy"], default=None, help=argparse.SUPPRESS)
     ap.add_argument("--cpu-seed", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-workload", choices=["a", "b", "c"], default="c", help=argparse.SUPPRESS)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL (one rank per GPU); gloo: a CPU-side rehearsal of the N > 1 path")
@@ -737,7 +767,8 @@ def main():
     args.xchg_gain = args.xchg_gain if args.xchg_gain is not None else c.get("xchg_gain", 2.0)
 
     if args.cpu_worker:                # a CPU-baseline child process: no GPU, one JSON line
-        print(json.dumps(cpu_worker(args.cpu_worker, args.cpu_seconds, args.config, args.cpu_seed)))
+        print(json.dumps(cpu_worker(args.cpu_worker, args.cpu_seconds, args.config, args.cpu_seed,
+                                    args.cpu_workload)))
         return
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # the driver's `bench.py --gpus N` without torch.distributed.run: one rank per GPU
@@ -904,6 +935,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.config, args.cpu_cores)
         out["cpu_baseline_numpy"] = cpu_baseline_numpy(min(args.cpu_seconds, 5.0), args.config, args.cpu_cores)
+        out["cpu_baseline_rollout"] = cpu_baseline_rollout(min(args.cpu_seconds, 4.0), args.config, args.cpu_cores)
+        out["cpu_baseline_rollout"]["gpu_rollout_only_hands_per_s"] = out["rollout_only_hands_per_s"]
     if rank == 0:
         emit_result(out)
     if dist is not None:

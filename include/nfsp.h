@@ -432,7 +432,7 @@ int nfsp_group_average_ar(nfsp_group* g);
  * replica order from +0, and W0 <- that.  every = 0: off.  NFSP_GROUP_AVG_AR at creation is
  * nets = AR, every = cfg.slices (once per step, after its last slice), scale = 1 / R.  The first
  * exchange of a net (or nfsp_group_average_ar) copies replica 0's net (with BR also its target
- * net) to every replica instead. */
+ * net) to every replica instead -- also the first after a call that turns the net on again. */
 #define NFSP_XCHG_AR 1u
 #define NFSP_XCHG_BR 2u
 int nfsp_group_set_exchange(nfsp_group* g, unsigned nets, int every, float scale);

@@ -811,9 +811,11 @@ static int update_impl(nfsp_engine* e, bool pipelined, int par, bool snap_after)
     }
     return NFSP_OK;
   };
-  // pipelined with the exchange: the BR chains first (they never wait for an exchange), then
-  // the previous call's exchange and this call's AR chain
-  const bool br_first = pipelined && e->xchg_every > 0 && !serial_ar;
+  // with the exchange on, the BR chains first (they never wait for an exchange), then the AR
+  // chain and the exchange (pipelined: the previous call's exchange, then this call's AR chain;
+  // else this call's, whose host transport synchronises the AR stream -- the BR streams are
+  // busy by then instead of waiting for the host)
+  const bool br_first = e->xchg_every > 0 && !serial_ar;
   if (br_first) {
     if ((rc = br_part()) != NFSP_OK) return rc;
     if ((rc = ar_part()) != NFSP_OK) return rc;
@@ -1035,7 +1037,12 @@ extern "C" int nfsp_group_set_exchange(nfsp_group* g, unsigned nets, int every, 
   NFSP_REQUIRE(g, "null argument");
   NFSP_REQUIRE((nets & ~(NFSP_XCHG_AR | NFSP_XCHG_BR)) == 0, "nets: NFSP_XCHG_AR | NFSP_XCHG_BR");
   NFSP_REQUIRE(every >= 0 && (every == 0 || nets), "every >= 0 (and nets when on)");
-  g->xchg_nets = every ? nets : 0;
+  // a net this call turns on starts like the rank path's (AvgPolicyExchange broadcasts rank 0's
+  // nets, then nfsp_engine_set_exchange takes them as W0): its next exchange copies replica 0's
+  // net everywhere instead of applying deltas against a W0 from before the exchange was off
+  const unsigned on = every ? nets : 0;
+  g->w0_valid &= ~(on & ~g->xchg_nets);
+  g->xchg_nets = on;
   g->xchg_every = every;
   g->xchg_scale = scale;
   g->calls = 0;

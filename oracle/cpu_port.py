@@ -21,7 +21,7 @@ class Cfg(C.Structure):
                 ("epsilon", C.c_double), ("eta", C.c_double),
                 ("batch", C.c_int32), ("target_every", C.c_int32),
                 ("seed", C.c_int64), ("init_seed", C.c_int64),
-                ("quirks", C.c_int32), ("game", C.c_int32)]
+                ("quirks", C.c_int32), ("game", C.c_int32), ("workload", C.c_int32)]
 
 
 class Stats(C.Structure):
@@ -59,14 +59,19 @@ def lib():
     return _lib
 
 
-def make_cfg(cfg=None, init_seed=0, quirks=True, game="leduc", rl_capacity=None, sl_capacity=None):
+WORKLOADS = {"c": 0, "a": 1, "b": 2}     # (c) end to end, (a) env + scheduler, (b) play
+
+
+def make_cfg(cfg=None, init_seed=0, quirks=True, game="leduc", rl_capacity=None, sl_capacity=None,
+             workload="c"):
     """nfsp_oracle.DEFAULT_CFG (+ overrides) as the C struct; both memories default to cfg buffer."""
     import nfsp_oracle as orc
     c = dict(orc.DEFAULT_CFG, **(cfg or {}))
     return Cfg(rl_capacity=rl_capacity or c["buffer"], sl_capacity=sl_capacity or c["buffer"],
                lr_br=c["lr_br"], lr_ar=c["lr_ar"], gamma=c["gamma"], epsilon=c["epsilon"],
                eta=c["eta"], batch=c["batch"], target_every=c["target_every"], seed=c["seed"],
-               init_seed=init_seed, quirks=int(bool(quirks)), game=1 if game == "kuhn" else 0)
+               init_seed=init_seed, quirks=int(bool(quirks)), game=1 if game == "kuhn" else 0,
+               workload=WORKLOADS[workload])
 
 
 class CpuGame:

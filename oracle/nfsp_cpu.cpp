@@ -492,6 +492,9 @@ typedef struct {
   int64_t init_seed;     // RandomState of the Glorot draws (nfsp_oracle.make_main)
   int32_t quirks;        // 1: the reference as written; 0: nfsp_oracle quirks=False
   int32_t game;          // 0 Leduc, 1 Kuhn
+  int32_t workload;      // BASELINE.md's CPU workloads: 0 (c) main.train end to end; 1 (a) env +
+                         // scheduler with uniform-random action vectors; 2 (b) Agent.play with
+                         // the MLP forwards and memory inserts, no update_strategy
 } nfsp_cpu_cfg;
 
 typedef struct {
@@ -678,12 +681,25 @@ struct Game {
       ++a.sl_inserts;
     }
     ++a.played;
-    if (a.game_step % 128 == 0) {                            // update_strategy
+    if (cfg.workload == 0 && a.game_step % 128 == 0) {     // update_strategy
       update_avg(a);
       update_br(a);
     }
     a.actions[act] += 1;
     return t;
+  }
+
+  // workload (a): a player that observes (Env.get_state) and steps the env with np.random.rand
+  // vectors -- main.train's scheduler around the env with no agent
+  bool play_random(int index, bool first) {
+    if (!first) {
+      (void)env.obs(index);
+      if (env.terminated) return true;
+    }
+    double at[3];
+    for (int q = 0; q < 3; ++q) at[q] = np.rand();
+    env.step(at, index);
+    return false;
   }
 
   void play_hand(int dealer) {                     // main.py:24-67
@@ -694,6 +710,16 @@ struct Game {
     pol[lhand] = py.random() > cfg.eta;
     uint32_t d_s = env.obs(dealer);
     bool first = true, d_t = false, l_t = false;
+    if (cfg.workload == 1) {
+      while (!(d_t && l_t)) {
+        int rnd = env.round;
+        if (!d_t) { d_t = play_random(dealer, first); first = false; }
+        if (!l_t) l_t = play_random(lhand, false);
+        if (rnd == env.round && !d_t) d_t = play_random(dealer, false);
+      }
+      ++hands;
+      return;
+    }
     while (!(d_t && l_t)) {
       int rnd = env.round;
       if (!d_t) { d_t = play(dealer, pol[dealer], dealer, first ? &d_s : nullptr); first = false; }

@@ -140,3 +140,29 @@ def test_rccl_transport_at_world_one(pkg):
         for key in rccl[0][k][0]:
             assert np.array_equal(rccl[0][k][0][key], host[0][k][0][key]), (k, key)
     assert _compare(rccl, _group(pkg, 1), 1) == 0.0
+
+
+def test_group_exchange_turned_on_again_starts_from_replica_0(pkg):
+    """nfsp_group_set_exchange turning the AR exchange on again (after steps with it off, the
+    replicas' AR nets apart) starts like the rank path does (rank 0's nets broadcast, then W0 =
+    them): the first exchange copies replica 0's nets everywhere, not W0_old + the deltas
+    accumulated since the exchange was off."""
+    import torch
+    g = pkg.engine.EngineGroup(2, seed=SEED, init_seed=INIT, **CFG)
+    g.set_exchange(pkg.native.XCHG_AR, every=1, scale=1.0)
+    g.step()
+    g.set_exchange(pkg.native.XCHG_AR, every=0)
+    g.step()
+    torch.cuda.synchronize()
+    w_r0 = [g.replicas[0].get_weights(a, 0) for a in (0, 1)]
+    assert not np.array_equal(w_r0[0], g.replicas[1].get_weights(0, 0))    # apart while off
+    g.set_exchange(pkg.native.XCHG_AR, every=1, scale=1.0)
+    g.average_ar()                                   # the exchange by itself
+    torch.cuda.synchronize()
+    for e in g.replicas:
+        for a in (0, 1):
+            assert np.array_equal(e.get_weights(a, 0), w_r0[a])
+    g.step()                                         # and it trains on from there
+    torch.cuda.synchronize()
+    assert np.array_equal(g.replicas[0].get_weights(0, 0), g.replicas[1].get_weights(0, 0))
+    g.close()
