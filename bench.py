@@ -106,6 +106,15 @@ CONFIGS = {
                               f"each with device M_RL 200k + M_SL 2M, target sync 150, reference cadence; "
                               f"AR nets averaged over the replicas every step")
        for R in (2, 4, 8, 16, 32, 64, 128, 256)},
+    # C4's arithmetic on ONE GPU (bench groups): R replicas of C4's per-GPU shard, the AR nets
+    # exchanged after every slice on device -- what --gpus R runs, in one process; trained from
+    # scratch over learn_steps steps (R x 1M hands each) beside the CPU band
+    **{f"c4_emul_r{R}": dict(n_lanes=R * 1_048_576, replicas=R, slices=128, slice_lag=2, rl_capacity=200_000,
+                             sl_capacity=2_000_000, xchg_every=1, xchg_gain=2.0, learn_steps=32 // R,
+                             label=f"C4 emulated on one GPU: {R} replicas x 1,048,576 Leduc lanes (128 pipelined "
+                                   f"slices each), M_RL 200k + M_SL 2M each, reference cadence; the replicas' AR "
+                                   f"nets exchanged after every slice (W0 + 2 x mean delta), from scratch")
+       for R in (4, 8)},
     "c5": dict(n_lanes=1_048_576, slices=16, slice_lag=2, rl_capacity=200_000, sl_capacity=2_000_000,
                game="kuhn", label="C5: Kuhn swap-in, 1,048,576 lanes/GPU (16 pipelined slices), C3's "
                                   "memories and cadence"),
@@ -568,35 +577,92 @@ def stub_main(args, world, rank, dist):
         dist.destroy_process_group()
 
 
+def cpu_band(hands: int) -> dict | None:
+    """The CPU reference's exact-exploitability seed band at `hands` hands (main.train restated
+    in C++ with C3's memories, 8 seeds, every 2M hands to 32M: tests/golden/cpu_band_c3mem.json),
+    at the nearest checkpoint; None past its last checkpoint."""
+    path = os.path.join(REPO, "tests", "golden", "cpu_band_c3mem.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        cb = json.load(f)["band"]
+    pts = sorted(int(k) for k in cb)
+    if hands > pts[-1] + (pts[1] - pts[0]) // 2:
+        return None
+    h = min(pts, key=lambda k: abs(k - hands))
+    return {"hands": h, "mean": cb[str(h)][0], "std": cb[str(h)][1],
+            "source": "tests/golden/cpu_band_c3mem.json (8 seeds)"}
+
+
+def band_check(x: float, hands: int) -> dict:
+    """One engine seed's exact exploitability against the CPU band at the same hands: the C3 /
+    C4 gates' bar (|x - mean| <= 2 sigma and x <= mean + sigma; the gates use 8 seeds)."""
+    b = cpu_band(hands)
+    out = {"hands": hands, "exploitability": x, "cpu_band": b}
+    if b is not None:
+        out["sigmas_from_cpu_mean"] = (x - b["mean"]) / b["std"]
+        out["inside_bar"] = abs(x - b["mean"]) <= 2 * b["std"] and x <= b["mean"] + b["std"]
+    return out
+
+
 def measure_group(pkg, name: str, steps: int, warmup: int) -> dict:
-    """A side measurement beside the headline (N = 1): engine-group config `name` (C3's
-    per-GPU lanes as R learner replicas, on-device AR exchange), W warmup + K un-instrumented
-    steps with the same sync protocol, and the exact exploitability after them.  The primary
-    figure is RL inserts/s: the learner's work follows the RL inserts (one update per 128),
-    and the inserts per hand grow as training goes on, so hands/s alone depends on the stage.
-    The stage is stated: the warmup is the headline's (W steps of 1,048,576 hands)."""
+    """A side measurement beside the headline (N = 1): engine-group config `name`, the same
+    sync protocol, and the exact exploitability of replica 0's AR nets (softmax mixed) against
+    the CPU reference's band at the same TOTAL hands (all replicas' hands: the replicas share
+    one AR net through the exchange).  Two forms:
+    * c3_rR: C3's per-GPU lanes as R learner replicas, AR nets averaged once per step; W warmup
+      + K timed steps (the stage is stated), exploitability after them;
+    * c4_emul_rR: BASELINE configs[3]'s arithmetic on one GPU -- R replicas of C4's per-GPU
+      shard (1,048,576 lanes in 128 pipelined slices, the AR nets exchanged after every slice,
+      W0 + gain x mean delta: the rank path bit for bit, tests/test_gpu_exchange.py), trained
+      from scratch for `learn_steps` steps, each step timed by itself and the exploitability
+      taken between steps outside the timing: hands/s and the learning curve over the same
+      hands."""
     import torch
     cfg = CONFIGS[name]
     R = cfg["replicas"]
-    g = pkg.engine.EngineGroup(R, n_lanes=cfg["n_lanes"] // R, rl_capacity=cfg["rl_capacity"],
-                               sl_capacity=cfg["sl_capacity"], seed=1234, init_seed=0, avg_ar=True)
-    for _ in range(warmup):
-        g.step()
-    torch.cuda.synchronize()
+    lanes = cfg["n_lanes"] // R
+    xchg = cfg.get("xchg_every")
+    extra = {k: cfg[k] for k in ("slices", "slice_lag") if k in cfg}
+    g = pkg.engine.EngineGroup(R, n_lanes=lanes, rl_capacity=cfg["rl_capacity"], sl_capacity=cfg["sl_capacity"],
+                               seed=1234, init_seed=0, avg_ar=not xchg, **extra)
+    out = {"workload": cfg["label"], "learner_replicas": R, "lanes_per_replica": lanes,
+           "metric": "hands/s (beside it RL inserts/s: M_RL inserts, each 1/128 of an update_strategy)",
+           "unit": "hands/s"}
     s0 = g.stats()
-    el = timed_steps(g.step, steps, 0, None, torch.cuda.synchronize)
+    if xchg:
+        g.set_exchange(pkg.native.XCHG_AR, every=xchg, scale=cfg["xchg_gain"] / R)
+        g.average_ar()                           # the ranks' broadcast: replica 0's AR nets
+        curve, el = [], 0.0
+        for k in range(cfg["learn_steps"]):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            g.step()
+            torch.cuda.synchronize()
+            el += time.perf_counter() - t0
+            curve.append(band_check(g.exploitability(0)["exploitability"], (k + 1) * cfg["n_lanes"]))
+        steps, warmup = cfg["learn_steps"], 0
+        out["learning_curve"] = curve
+        out["inside_bar_at_every_checkpoint"] = all(c.get("inside_bar", False) for c in curve)
+        out["timing"] = "each step bracketed by device syncs from scratch; evaluations between steps untimed"
+    else:
+        for _ in range(warmup):
+            g.step()
+        torch.cuda.synchronize()
+        s0 = g.stats()
+        el = timed_steps(g.step, steps, 0, None, torch.cuda.synchronize)
     s1 = g.stats()
     hands = steps * cfg["n_lanes"]
     rl = sum(s1["rl_total"]) - sum(s0["rl_total"])
-    out = {"workload": cfg["label"], "learner_replicas": R, "lanes_per_replica": cfg["n_lanes"] // R,
-           "metric": "hands/s (beside it RL inserts/s: M_RL inserts, each 1/128 of an update_strategy)",
-           "value": hands / el, "unit": "hands/s", "hands_per_s": hands / el,
-           "training_stage": {"warmup_steps": warmup, "hands_before_timing": warmup * cfg["n_lanes"]},
-           "steps": steps, "warmup": warmup,
-           "ms_per_step": el / steps * 1e3, "rl_inserts_per_s": rl / el,
-           "rl_inserts_per_hand": rl / hands,
-           "exploitability_exact_softmax": g.exploitability(0)["exploitability"],
-           "hands_trained": int(s1["hands"])}
+    ex = g.exploitability(0)["exploitability"]
+    out.update({"value": hands / el, "hands_per_s": hands / el,
+                "training_stage": {"warmup_steps": warmup, "hands_before_timing": warmup * cfg["n_lanes"]},
+                "steps": steps, "warmup": warmup,
+                "ms_per_step": el / steps * 1e3, "rl_inserts_per_s": rl / el,
+                "rl_inserts_per_hand": rl / hands,
+                "exploitability_exact_softmax": ex,
+                "exploitability_vs_cpu_band": band_check(ex, int(s1["hands"])),
+                "hands_trained": int(s1["hands"])})
     g.close()
     del g
     torch.cuda.empty_cache()
@@ -756,13 +822,15 @@ def main():
     ap.add_argument("--slices", type=int, default=None, help="override the config's lane slices")
     ap.add_argument("--slice-lag", type=int, default=None, choices=[1, 2],
                     help="override the config's slice lag (2: slices pipelined)")
-    ap.add_argument("--groups", default="c3_r4,c3_r16,c3_r64,c3_r256",
+    ap.add_argument("--groups", default="c4_emul_r8,c3_r4,c3_r16,c3_r64,c3_r256",
                     help="engine-group configs measured beside the C3 headline at N = 1 "
                          "(`groups` in the JSON line; '' = none)")
     args = ap.parse_args()
     if args.config is None:
         args.config = "c4" if max(args.gpus, int(os.environ.get("WORLD_SIZE", "1"))) > 1 else "c3"
     c = CONFIGS[args.config]
+    if "learn_steps" in c:
+        ap.error(f"{args.config} is a one-GPU group line: bench.py --groups {args.config}")
     args.xchg_every = args.xchg_every if args.xchg_every is not None else c.get("xchg_every", 1)
     args.xchg_gain = args.xchg_gain if args.xchg_gain is not None else c.get("xchg_gain", 2.0)
 
@@ -915,16 +983,9 @@ def main():
     out["exploitability_exact"] = {
         "softmax_mixed": ex[0]["exploitability"], "argmax_as_executed": ex[1]["exploitability"],
         "hands_trained_per_gpu": int(s2["hands"]), "unit": "chips (BR_0 + BR_1)"}
-    band_path = os.path.join(REPO, "tests", "golden", "cpu_band_c3mem.json")
-    if cfg.get("game", "leduc") == "leduc" and cfg["rl_capacity"] == 200_000 and os.path.exists(band_path):
-        # the CPU reference's seed band at the same hands (main.train in C++, C3's memories,
-        # 8 seeds: tests/golden/cpu_band_c3mem.json; one seed of the engine here)
-        with open(band_path) as f:
-            cb = json.load(f)["band"]
-        h = min((int(k) for k in cb), key=lambda k: abs(k - int(s2["hands"])))
-        out["exploitability_exact"]["cpu_band_at_hands"] = {
-            "hands": h, "mean": cb[str(h)][0], "std": cb[str(h)][1],
-            "source": "tests/golden/cpu_band_c3mem.json (8 seeds)"}
+    if cfg.get("game", "leduc") == "leduc" and cfg["rl_capacity"] == 200_000:
+        # the CPU reference's seed band at the same hands (one seed of the engine here)
+        out["exploitability_exact"]["vs_cpu_band"] = band_check(ex[0]["exploitability"], int(s2["hands"]))
     if world == 1 and args.config == "c3" and args.groups:
         # several learners on the one GPU (engine groups): new measured configs, not the headline
         eng.close()
