@@ -22,6 +22,7 @@ import pytest
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 pytestmark = pytest.mark.gpu
 
+# 8 slices of 8,192 lanes: the slice size of C4's shard (1,048,576 lanes in 128 slices, bench.CONFIGS["c4"])
 CFG = dict(n_lanes=65_536, slices=8, slice_lag=2, rl_capacity=40_000, sl_capacity=60_000, target_every=40)
 SEED, INIT = 777, 5
 STEPS = 2
