@@ -13,7 +13,7 @@ import pytest
 
 from conftest import REPO
 
-PROFILES = [("r04_bench_measure.json", "c3"), ("r03_bench_default.json", "c3"), ("r03_c2_bench.json", "c2"),
+PROFILES = [("r05_bench_driver_cmd.json", "c3"), ("r04_bench_measure.json", "c3"), ("r03_bench_default.json", "c3"), ("r03_c2_bench.json", "c2"),
             ("r03_c5_bench.json", "c5"), ("r03_c5_tb_bench.json", "c5_tb")]
 
 
@@ -83,7 +83,8 @@ def test_c3_rollout_frac_reproduces_from_the_kernel_stats():
 
 
 @pytest.mark.parametrize("line,stats", [("r04_bench_measure.json", "r04_c3_kernel_stats.csv"),
-                                        ("r04_driver_cmd_prof_bench.json", "r04_driver_cmd_kernel_stats.csv")])
+                                        ("r04_driver_cmd_prof_bench.json", "r04_driver_cmd_kernel_stats.csv"),
+                                        ("r05_driver_cmd_prof_bench.json", "r05_driver_cmd_kernel_stats.csv")])
 def test_c3_dominant_chain_duration_agrees_with_rocprof(line, stats):
     """The headline's roofline kernel (the chain on the critical stream) has the same average
     launch duration in bench's live HIP-event pass and in the rocprofv3 kernel statistics of the
@@ -105,3 +106,16 @@ def test_cpu_share_is_bounded_by_the_machine():
     import bench
     n = bench.cpu_share()
     assert 1 <= n <= (os.cpu_count() or 1)
+
+
+def test_cpu_band_lookup_matches_the_learning_gates():
+    """The group lines' band comparison (bench.band_check) uses the CPU band as the C3 / C4
+    gates do: the nearest checkpoint, and past the band's last one (32M) that one, flagged."""
+    import bench
+    b = bench.cpu_band(8_388_608)
+    assert b["hands"] == 8_000_000 and "beyond_band" not in b
+    for h in (33_554_432, 67_108_864):
+        b = bench.cpu_band(h)
+        assert b["hands"] == 32_000_000 and b["beyond_band"] is True
+    c = bench.band_check(1.0, 33_554_432)
+    assert c["inside_bar"] is True and c["cpu_band"]["beyond_band"] is True
