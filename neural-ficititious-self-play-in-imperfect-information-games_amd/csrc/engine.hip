@@ -258,6 +258,20 @@ __global__ void __launch_bounds__(256) k_group_snap(const GroupRollout* __restri
     for (int p = p0; p <= p1; ++p) T.snap_eps[2 * p + threadIdx.x] = T.A.st->epsilon[threadIdx.x];
 }
 
+// The same for a pipelined group step (nfsp_group_step, slice_lag 2): the nets of one learner
+// stream only, on that stream right after its chains -- part 0: both agents' AR nets (after
+// the AR chains and the exchange); part 1: the BR and target nets and the epsilons (after the
+// BR chains and their k_finalize).  Together the two write what k_group_snap writes.
+__global__ void __launch_bounds__(256) k_group_snap_part(const GroupRollout* __restrict__ tab, int par, int part) {
+  const GroupRollout& T = tab[blockIdx.y];
+  float* const dst = T.snap + (size_t)par * 6 * nn::NP;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < 6 * nn::NP; i += gridDim.x * blockDim.x) {
+    const int net = (i / nn::NP) % 3;            // [agent][AR, BR, target][NP]
+    if ((net == 0) == (part == 0)) dst[i] = T.A.w[i];
+  }
+  if (part == 1 && blockIdx.x == 0 && threadIdx.x < 2) T.snap_eps[2 * par + threadIdx.x] = T.A.st->epsilon[threadIdx.x];
+}
+
 // ---------------------------------------------------------------------------
 // scan of the 4 per-lane counts (canonical insert order)
 // ---------------------------------------------------------------------------
@@ -601,7 +615,7 @@ int engine_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, bool own_streams, n
   // (cfg.slice_lag 2: two sets, slice parity; the reservoir lists are shared -- only the
   // ctx stream's prep kernels use them, in slice order)
   e->slice_lag = cfg->slice_lag;
-  for (int k = 0; k < (e->slice_lag == 2 && own_streams ? 2 : 1); ++k) {
+  for (int k = 0; k < (e->slice_lag == 2 ? 2 : 1); ++k) {   // (group replicas too: pipelined groups)
     LearnBufs& L = e->LBs[k];
     L.umax = 4 * N / cfg->inserts_per_update + 2;
     const int64_t ub = 2 * L.umax * cfg->batch, ueb = ub * cfg->epochs;
@@ -778,6 +792,13 @@ int group_rollout_launch(nfsp_engine* const* eng, int R, const void* d_tab, int 
     eng[r]->rollouts++;
     eng[r]->pending_update = true;
   }
+  return NFSP_OK;
+}
+
+int group_snap_part_launch(nfsp_engine* const* eng, int R, const void* d_tab, int par, int part, hipStream_t s) {
+  k_group_snap_part<<<dim3(nfsp_blocks(6 * nn::NP, 256), R), 256, 0, s>>>(static_cast<const GroupRollout*>(d_tab),
+                                                                         par, part);
+  NFSP_LAUNCHED("k_group_snap_part");
   return NFSP_OK;
 }
 

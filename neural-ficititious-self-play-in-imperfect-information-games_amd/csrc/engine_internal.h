@@ -316,6 +316,8 @@ int group_rollout_table(nfsp_engine* const* eng, int R, void** d_tab);
 int group_rollout_launch(nfsp_engine* const* eng, int R, const void* d_tab, int par);
 // slice_lag 2: every replica's nets and epsilon -> snapshot par (-1: both parities)
 int group_snap_launch(nfsp_engine* const* eng, int R, const void* d_tab, int par);
+// one learner stream's part of it (0: AR nets; 1: BR / target nets and epsilons) on stream s
+int group_snap_part_launch(nfsp_engine* const* eng, int R, const void* d_tab, int par, int part, hipStream_t s);
 // the cross-shard exchange of the AR nets, enqueued on `s` (the AR chain stream)
 int exchange_enqueue(nfsp_engine* e, hipStream_t s);
 

@@ -898,10 +898,13 @@ struct nfsp_group {
   std::vector<nfsp_engine*> eng;
   hipStream_t s_ar = nullptr, s_br = nullptr;
   void* d_roll = nullptr;        // the replicas' rollout arguments (static device table)
-  // per learner call: job / prep / final tables, host (pinned) staging -> device, one copy
-  char* h_tab = nullptr;
-  char* d_tab = nullptr;
-  size_t tab_cap = 0;
+  // per learner call: job / prep / final tables, host (pinned) staging -> device, one copy;
+  // two sets by slice parity (a pipelined step's slice j + 1 fills its set while slice j's
+  // chains still read theirs)
+  char* h_tab[2] = {nullptr, nullptr};
+  char* d_tab[2] = {nullptr, nullptr};
+  size_t tab_cap[2] = {0, 0};
+  hipEvent_t snap_ev[2][2] = {};  // pipelined step: [parity][AR, BR stream] snapshot copies done
   // the replicas' EngineDev, gathered on device and read back in one copy
   EngineDev** d_stp = nullptr;   // [R] -> each replica's state
   EngineDev* d_st = nullptr;     // [R]
@@ -936,9 +939,14 @@ extern "C" int nfsp_group_destroy(nfsp_group* g) {
   for (hipStream_t st : {g->s_ar, g->s_br})
     if (st) (void)hipStreamSynchronize(st);
   for (nfsp_engine* e : g->eng) nfsp_engine_destroy(e);
-  if (g->h_tab) (void)hipHostFree(g->h_tab);
+  for (int p = 0; p < 2; ++p) {
+    if (g->h_tab[p]) (void)hipHostFree(g->h_tab[p]);
+    if (g->d_tab[p]) (void)hipFree(g->d_tab[p]);
+    for (hipEvent_t ev : g->snap_ev[p])
+      if (ev) (void)hipEventDestroy(ev);
+  }
   if (g->h_st) (void)hipHostFree(g->h_st);
-  for (void* p : {(void*)g->d_tab, (void*)g->d_war, (void*)g->w0, g->d_roll, (void*)g->d_stp, (void*)g->d_st})
+  for (void* p : {(void*)g->d_war, (void*)g->w0, g->d_roll, (void*)g->d_stp, (void*)g->d_st})
     if (p) (void)hipFree(p);
   for (hipStream_t st : {g->s_ar, g->s_br})
     if (st) (void)hipStreamDestroy(st);
@@ -986,6 +994,14 @@ extern "C" int nfsp_group_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, int 
       return nfsp::hip_fail(sr, "nfsp_group_create: hipStreamCreate");
     }
   }
+  for (auto& pe : g->snap_ev)
+    for (hipEvent_t& ev : pe) {
+      const hipError_t er = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+      if (er != hipSuccess) {
+        nfsp_group_destroy(g);
+        return nfsp::hip_fail(er, "nfsp_group_create: hipEventCreate");
+      }
+    }
   int rc = nfsp::eng::group_rollout_table(g->eng.data(), replicas, &g->d_roll);
   if (rc != NFSP_OK) {
     nfsp_group_destroy(g);
@@ -1019,18 +1035,22 @@ extern "C" int nfsp_group_engine(nfsp_group* g, int r, nfsp_engine** out) {
   return NFSP_OK;
 }
 
-extern "C" int nfsp_group_average_ar(nfsp_group* g) {
-  NFSP_REQUIRE(g, "null argument");
+// the group's exchange (k_group_xchg) on stream `s`
+static int group_xchg_launch(nfsp_group* g, hipStream_t s) {
   const unsigned nets = g->xchg_nets ? g->xchg_nets : NFSP_XCHG_AR;
   // nets not broadcast yet take replica 0's (a BR net with its target net)
   unsigned bc = nets & ~g->w0_valid;
   if (bc & NFSP_XCHG_BR) bc |= 4u;
   const float scale = g->xchg_nets ? g->xchg_scale : 1.0f / (float)g->R;
-  k_group_xchg<<<nfsp_blocks(3 * 2 * nn::NP, 256), 256, 0, g->ctx->stream>>>(g->d_war, g->w0, g->R, nets,
-                                                                            bc, scale);
+  k_group_xchg<<<nfsp_blocks(3 * 2 * nn::NP, 256), 256, 0, s>>>(g->d_war, g->w0, g->R, nets, bc, scale);
   NFSP_LAUNCHED("k_group_xchg");
   g->w0_valid |= nets;
   return NFSP_OK;
+}
+
+extern "C" int nfsp_group_average_ar(nfsp_group* g) {
+  NFSP_REQUIRE(g, "null argument");
+  return group_xchg_launch(g, g->ctx->stream);
 }
 
 extern "C" int nfsp_group_set_exchange(nfsp_group* g, unsigned nets, int every, float scale) {
@@ -1060,7 +1080,13 @@ struct TabCursor {
   }
 };
 
-static int group_update(nfsp_group* g) {
+// One learner call of every replica for their pending rollouts.  par: the learner-buffer and
+// table set (slice parity; 0 unless pipelined).  pipelined (nfsp_group_step at slice_lag 2):
+// nothing joins the ctx stream -- the counters are published on it after the prep, the BR
+// results on the BR stream after the last round; the exchange (when due) follows the AR chains
+// on the AR stream; with snap_after each learner stream then copies its nets into snapshot
+// `par` and records snap_ev[par] for the rollout two slices on.
+static int group_update(nfsp_group* g, bool pipelined = false, int par = 0, bool snap_after = false) {
   hipStream_t s = g->ctx->stream;
   const int R = g->R;
   nfsp_engine* e0 = g->eng[0];
@@ -1079,6 +1105,7 @@ static int group_update(nfsp_group* g) {
   for (int r = 0; r < R; ++r) {
     nfsp_engine* e = g->eng[r];
     NFSP_REQUIRE(e->log_loss == loss_log, "the loss log must be on in all replicas of a group or none");
+    e->LB = e->LBs[par];
     if ((rc = plan_update(e, g->h_st[r], L[r])) != NFSP_OK) return rc;
     maxU = L[r].maxU > maxU ? L[r].maxU : maxU;
     maxUbr = L[r].maxUbr > maxUbr ? L[r].maxUbr : maxUbr;
@@ -1124,33 +1151,39 @@ static int group_update(nfsp_group* g) {
   const size_t o_ar = cur.take<ChainJob>(ar_jobs.size()), o_br = cur.take<ChainJob>(br_jobs.size());
   const size_t o_tg = cur.take<TargetJob>(tg_jobs.size());
   const size_t need = cur.off;
-  if (need > g->tab_cap) {     // every earlier use of the tables completed (the sync above)
-    if (g->h_tab) NFSP_HIP(hipHostFree(g->h_tab));
-    if (g->d_tab) NFSP_HIP(hipFree(g->d_tab));
-    g->h_tab = nullptr;
-    g->d_tab = nullptr;
-    g->tab_cap = 0;
+  // Every earlier use of set `par` has completed: serially, the call starts with the readback's
+  // sync; pipelined, the ctx stream waited for slice j - 2's snapshot events (after its chains)
+  // before this slice's rollout.  A grown set is freed and reallocated: the device free
+  // synchronises the device.
+  char*& h_tab = g->h_tab[par];
+  char*& d_tab = g->d_tab[par];
+  if (need > g->tab_cap[par]) {
+    if (h_tab) NFSP_HIP(hipHostFree(h_tab));
+    if (d_tab) NFSP_HIP(hipFree(d_tab));
+    h_tab = nullptr;
+    d_tab = nullptr;
+    g->tab_cap[par] = 0;
     const size_t cap = need * 2;
-    NFSP_HIP(hipHostMalloc((void**)&g->h_tab, cap, hipHostMallocDefault));
-    NFSP_HIP(hipMalloc((void**)&g->d_tab, cap));
-    g->tab_cap = cap;
+    NFSP_HIP(hipHostMalloc((void**)&h_tab, cap, hipHostMallocDefault));
+    NFSP_HIP(hipMalloc((void**)&d_tab, cap));
+    g->tab_cap[par] = cap;
   }
   for (int r = 0; r < R; ++r) {
-    memcpy(g->h_tab + o_prep + sizeof(PrepArgs) * r, &L[r].P, sizeof(PrepArgs));
-    memcpy(g->h_tab + o_fin + sizeof(FinalArgs) * r, &L[r].F, sizeof(FinalArgs));
+    memcpy(h_tab + o_prep + sizeof(PrepArgs) * r, &L[r].P, sizeof(PrepArgs));
+    memcpy(h_tab + o_fin + sizeof(FinalArgs) * r, &L[r].F, sizeof(FinalArgs));
   }
-  memcpy(g->h_tab + o_ar, ar_jobs.data(), sizeof(ChainJob) * ar_jobs.size());
-  memcpy(g->h_tab + o_br, br_jobs.data(), sizeof(ChainJob) * br_jobs.size());
-  memcpy(g->h_tab + o_tg, tg_jobs.data(), sizeof(TargetJob) * tg_jobs.size());
-  const PrepArgs* d_prep = reinterpret_cast<const PrepArgs*>(g->d_tab + o_prep);
-  const FinalArgs* d_fin = reinterpret_cast<const FinalArgs*>(g->d_tab + o_fin);
-  const ChainJob* d_ar = reinterpret_cast<const ChainJob*>(g->d_tab + o_ar);
-  const ChainJob* d_br = reinterpret_cast<const ChainJob*>(g->d_tab + o_br);
-  const TargetJob* d_tg = reinterpret_cast<const TargetJob*>(g->d_tab + o_tg);
+  memcpy(h_tab + o_ar, ar_jobs.data(), sizeof(ChainJob) * ar_jobs.size());
+  memcpy(h_tab + o_br, br_jobs.data(), sizeof(ChainJob) * br_jobs.size());
+  memcpy(h_tab + o_tg, tg_jobs.data(), sizeof(TargetJob) * tg_jobs.size());
+  const PrepArgs* d_prep = reinterpret_cast<const PrepArgs*>(d_tab + o_prep);
+  const FinalArgs* d_fin = reinterpret_cast<const FinalArgs*>(d_tab + o_fin);
+  const ChainJob* d_ar = reinterpret_cast<const ChainJob*>(d_tab + o_ar);
+  const ChainJob* d_br = reinterpret_cast<const ChainJob*>(d_tab + o_br);
+  const TargetJob* d_tg = reinterpret_cast<const TargetJob*>(d_tab + o_tg);
   hipEvent_t fork_br = take_event(e0), fork = take_event(e0);
   {
     KTimer kprep(e0, KT_PREP);
-    NFSP_HIP(hipMemcpyAsync(g->d_tab, g->h_tab, need, hipMemcpyHostToDevice, s));
+    NFSP_HIP(hipMemcpyAsync(d_tab, h_tab, need, hipMemcpyHostToDevice, s));
     // the same prep kernels as one engine's, every replica in one launch (blockIdx.z)
     if (maxUbr > 0) {
       k_br_prep<1><<<dim3((unsigned)maxUbr, 2, R), 128, 0, s>>>(PrepArgs{}, d_prep);
@@ -1180,6 +1213,10 @@ static int group_update(nfsp_group* g) {
       k_res_apply<1><<<dim3(nfsp_blocks(maxSL, 256), 2, R), 256, 0, s>>>(PrepArgs{}, d_prep);
       NFSP_LAUNCHED("k_res_apply");
     }
+  }
+  if (pipelined) {                     // the counters, before the next rollout's commit
+    k_finalize<1><<<R, 64, 0, s>>>(FinalArgs{}, d_fin, 1);
+    NFSP_LAUNCHED("k_finalize");
   }
   // When chains share CUs (R > 64), the first round's BR targets run before the AR chains
   // start: alone they take the chip's issue slots instead of competing with 2R resident AR
@@ -1227,6 +1264,26 @@ static int group_update(nfsp_group* g) {
     if ((rc = launch_br_chain(C, nj, cfg.quirks, loss_log, g->s_br)) != NFSP_OK) return rc;
   }
   if (!ar_launched && (rc = launch_ar(nullptr)) != NFSP_OK) return rc;
+  if (pipelined) {
+    // BR stream: the replicas' BR results, then (snap_after) their BR / target nets and
+    // epsilons into snapshot `par`
+    k_finalize<1><<<R, 64, 0, g->s_br>>>(FinalArgs{}, d_fin, 6);
+    NFSP_LAUNCHED("k_finalize");
+    // AR stream: the exchange when due (after this call's AR chains; AR nets only, so no other
+    // stream touches what it writes), then the AR nets into snapshot `par`
+    NFSP_HIP(hipStreamWaitEvent(g->s_ar, fork, 0));
+    if (g->xchg_every > 0 && (++g->calls) % g->xchg_every == 0 && (rc = group_xchg_launch(g, g->s_ar)) != NFSP_OK)
+      return rc;
+    if (snap_after) {
+      if ((rc = nfsp::eng::group_snap_part_launch(g->eng.data(), R, g->d_roll, par, 1, g->s_br)) != NFSP_OK) return rc;
+      NFSP_HIP(hipEventRecord(g->snap_ev[par][1], g->s_br));
+      if ((rc = nfsp::eng::group_snap_part_launch(g->eng.data(), R, g->d_roll, par, 0, g->s_ar)) != NFSP_OK) return rc;
+      NFSP_HIP(hipEventRecord(g->snap_ev[par][0], g->s_ar));
+    }
+    e0->pool.push_back(fork);
+    e0->pool.push_back(fork_br);
+    return NFSP_OK;
+  }
   for (hipStream_t st : {g->s_ar, g->s_br}) {
     hipEvent_t j = take_event(e0);
     NFSP_HIP(hipEventRecord(j, st));
@@ -1292,6 +1349,29 @@ extern "C" int nfsp_group_step(nfsp_group* g) {
     if ((rc = nfsp_group_average_ar(g)) != NFSP_OK) return rc;
   const int K = g->eng[0]->slices;
   const bool lag2 = g->eng[0]->slice_lag == 2 && K > 1;
+  // Pipelined (as step_pipelined): slice j's rollout waits only for the snapshot copies of
+  // slice j - 2, so the rollout, readback, plan and prep of slice j + 1 overlap slice j's
+  // chains.  The same arithmetic as the serial loop below.  Not with a BR exchange (it would
+  // need both learner streams joined after every exchange) or NFSP_GROUP_SERIAL=1.
+  static const bool serial_env = getenv("NFSP_GROUP_SERIAL") && atoi(getenv("NFSP_GROUP_SERIAL"));
+  if (lag2 && !(g->xchg_nets & NFSP_XCHG_BR) && !serial_env) {
+    hipStream_t s = g->ctx->stream;
+    if ((rc = nfsp::eng::group_snap_launch(g->eng.data(), g->R, g->d_roll, -1)) != NFSP_OK) return rc;
+    for (int j = 0; j < K; ++j) {
+      const int par = j & 1;
+      if (j >= 2)
+        for (hipEvent_t ev : g->snap_ev[par]) NFSP_HIP(hipStreamWaitEvent(s, ev, 0));
+      if ((rc = nfsp::eng::group_rollout_launch(g->eng.data(), g->R, g->d_roll, par)) != NFSP_OK) return rc;
+      if ((rc = group_update(g, true, par, j + 2 < K)) != NFSP_OK) return rc;
+    }
+    for (hipStream_t st : {g->s_ar, g->s_br}) {    // the step ends with every stream joined
+      hipEvent_t jv = take_event(g->eng[0]);
+      NFSP_HIP(hipEventRecord(jv, st));
+      NFSP_HIP(hipStreamWaitEvent(s, jv, 0));
+      g->eng[0]->pool.push_back(jv);
+    }
+    return NFSP_OK;
+  }
   if (lag2 && (rc = nfsp::eng::group_snap_launch(g->eng.data(), g->R, g->d_roll, -1)) != NFSP_OK) return rc;
   for (int j = 0; j < K; ++j) {
     if ((rc = nfsp::eng::group_rollout_launch(g->eng.data(), g->R, g->d_roll, lag2 ? (j & 1) : -1)) != NFSP_OK)

@@ -29,6 +29,7 @@ int engine_create(nfsp_ctx*, const nfsp_engine_cfg*, bool, nfsp_engine**) { retu
 int group_rollout_table(nfsp_engine* const*, int, void**) { return NFSP_EINVAL; }
 int group_rollout_launch(nfsp_engine* const*, int, const void*, int) { return NFSP_EINVAL; }
 int group_snap_launch(nfsp_engine* const*, int, const void*, int) { return NFSP_EINVAL; }
+int group_snap_part_launch(nfsp_engine* const*, int, const void*, int, int, hipStream_t) { return NFSP_EINVAL; }
 int exchange_enqueue(nfsp_engine*, hipStream_t) { return NFSP_EINVAL; }
 int rollout_launch_with(nfsp_engine*, const float*, const double*) { return NFSP_EINVAL; }
 }
