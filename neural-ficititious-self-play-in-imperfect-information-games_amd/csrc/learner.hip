@@ -1126,25 +1126,53 @@ static int group_update(nfsp_group* g, bool pipelined = false, int par = 0, bool
   for (int r = 0; r < R; ++r)
     for (int a = 0; a < 2; ++a)
       if (L[r].P.A[a].U > 0) ar_jobs.push_back(ar_job(g->eng[r], L[r], a));
-  size_t rounds = 0;
+  // BR rounds: round k = one k_br_targets launch (the targets of the segments that start in
+  // it, whole segments) + one chain launch (every (replica, agent) with BR work left: the next
+  // piece of its current segment, at most `cap` updates; a target sync ends the last piece of
+  // its segment).  cap 0: one round per segment index, every job's k-th segment in round k.
+  // A round lasts as long as its longest piece, so with whole segments the round structure
+  // waits for the longest segment of every round: a sliced group's BR stream ran 1.9 ms per
+  // slice against 1.2 ms for its busiest job (tools/group_timeline.py).  Pieces of a segment
+  // resume from the weights in memory: the same SGD steps, bit for bit.
+  static const int cap_env = getenv("NFSP_GROUP_BR_CAP") ? atoi(getenv("NFSP_GROUP_BR_CAP")) : -1;
+  const int64_t cap = cap_env >= 0 ? cap_env : (e0->slices > 1 ? 40 : 0);
+  struct BrCursor {
+    int r, a;
+    size_t s;        // current segment
+    int64_t pos;     // next update of it
+  };
+  std::vector<BrCursor> bc;
   for (int r = 0; r < R; ++r)
-    for (int a = 0; a < 2; ++a) rounds = L[r].seg[a].size() > rounds ? L[r].seg[a].size() : rounds;
+    for (int a = 0; a < 2; ++a)
+      if (!L[r].seg[a].empty()) bc.push_back({r, a, 0, L[r].seg[a][0].u});
   std::vector<ChainJob> br_jobs;
   std::vector<TargetJob> tg_jobs;
-  std::vector<size_t> round_off(rounds + 1, 0);
-  std::vector<int64_t> round_n(rounds, 0);
-  for (size_t k = 0; k < rounds; ++k) {
-    round_off[k] = br_jobs.size();
-    for (int r = 0; r < R; ++r)
-      for (int a = 0; a < 2; ++a)
-        if (k < L[r].seg[a].size()) {
-          const Segment& sg = L[r].seg[a][k];
-          br_jobs.push_back(br_chain_job(g->eng[r], a, sg));
-          tg_jobs.push_back(br_target_job(g->eng[r], L[r], a, sg));
-          round_n[k] = sg.v - sg.u > round_n[k] ? sg.v - sg.u : round_n[k];
-        }
+  std::vector<size_t> br_off, tg_off;
+  std::vector<int64_t> round_n;          // the longest starting segment of each round (targets grid)
+  for (;;) {
+    const size_t b0 = br_jobs.size(), t0 = tg_jobs.size();
+    int64_t rn = 0;
+    for (BrCursor& c : bc) {
+      const std::vector<Segment>& segs = L[c.r].seg[c.a];
+      if (c.s >= segs.size()) continue;
+      const Segment& sg = segs[c.s];
+      if (c.pos == sg.u) {
+        tg_jobs.push_back(br_target_job(g->eng[c.r], L[c.r], c.a, sg));
+        rn = sg.v - sg.u > rn ? sg.v - sg.u : rn;
+      }
+      const int64_t end = cap > 0 && c.pos + cap < sg.v ? c.pos + cap : sg.v;
+      br_jobs.push_back(br_chain_job(g->eng[c.r], c.a, Segment{c.pos, end, sg.sync && end == sg.v}));
+      c.pos = end;
+      if (end == sg.v && ++c.s < segs.size()) c.pos = segs[c.s].u;
+    }
+    if (br_jobs.size() == b0) break;
+    br_off.push_back(b0);
+    tg_off.push_back(t0);
+    round_n.push_back(rn);
   }
-  round_off[rounds] = br_jobs.size();
+  const size_t rounds = round_n.size();
+  br_off.push_back(br_jobs.size());
+  tg_off.push_back(tg_jobs.size());
   g->rounds = (int64_t)rounds;
   TabCursor cur;
   const size_t o_prep = cur.take<PrepArgs>(R), o_fin = cur.take<FinalArgs>(R);
@@ -1241,13 +1269,16 @@ static int group_update(nfsp_group* g, bool pipelined = false, int par = 0, bool
   NFSP_HIP(hipStreamWaitEvent(g->s_br, fork_br, 0));
   KTimer kspan(e0, KT_BR_STREAM0, g->s_br);     // the group's one BR stream, end to end
   for (size_t k = 0; k < rounds; ++k) {
-    const int nj = (int)(round_off[k + 1] - round_off[k]);
-    {
-      KTimer kt2(e0, KT_TARGETS, g->s_br);
-      k_br_targets<<<dim3((unsigned)round_n[k], (unsigned)nj), 256, 0, g->s_br>>>(
-          d_tg + round_off[k], TargetJob{}, cfg.batch, cfg.epochs, cfg.gamma, cfg.quirks, cfg.lr_br);
+    const int nj = (int)(br_off[k + 1] - br_off[k]);
+    const int nt = (int)(tg_off[k + 1] - tg_off[k]);
+    if (nt > 0) {
+      {
+        KTimer kt2(e0, KT_TARGETS, g->s_br);
+        k_br_targets<<<dim3((unsigned)round_n[k], (unsigned)nt), 256, 0, g->s_br>>>(
+            d_tg + tg_off[k], TargetJob{}, cfg.batch, cfg.epochs, cfg.gamma, cfg.quirks, cfg.lr_br);
+      }
+      NFSP_LAUNCHED("k_br_targets");
     }
-    NFSP_LAUNCHED("k_br_targets");
     if (!ar_launched) {
       hipEvent_t t0 = take_event(e0);
       NFSP_HIP(hipEventRecord(t0, g->s_br));
@@ -1256,7 +1287,7 @@ static int group_update(nfsp_group* g, bool pipelined = false, int par = 0, bool
       ar_launched = true;
     }
     ChainArgs C{};
-    C.jobs = d_br + round_off[k];
+    C.jobs = d_br + br_off[k];
     C.B = cfg.batch;
     C.E = cfg.epochs;
     C.lds = g->chain_lds;

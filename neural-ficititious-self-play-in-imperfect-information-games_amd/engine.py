@@ -264,7 +264,9 @@ class EngineGroup:
     launches.  ``avg_ar``: the AR nets are averaged over the replicas after every step (C4's
     exchange on device, shards.AvgPolicyAllReduce); ``set_exchange`` for other cadences (e.g.
     after every slice, shards.AvgPolicyExchange's).  ``slice_lag=2``: every replica's slice j
-    acts with the nets slice j - 2 left (a pipelined engine's arithmetic, run serially)."""
+    acts with the nets slice j - 2 left (a pipelined engine's arithmetic; executed pipelined --
+    slice j + 1's rollout, plan and prep overlap slice j's chains -- unless the BR nets are
+    exchanged or NFSP_GROUP_SERIAL=1)."""
 
     def __init__(self, replicas: int, ctx: native.Context | None = None, init_seed: int = 0,
                  game: int = native.GAME_LEDUC, avg_ar: bool = False, **cfg):
