@@ -19,8 +19,6 @@
 // BR chains are cut into segments at target-sync points; the two agents' BR chains and
 // the AR chains run on separate streams.
 #include <math.h>
-#include <stdio.h>
-#include <string>
 #include <stdlib.h>
 #include <string.h>
 
@@ -289,164 +287,88 @@ struct TargetJob {
 __global__ void __launch_bounds__(256) k_br_targets(const TargetJob* __restrict__ jobs, TargetJob one,
                                                     int B, int E, double gamma, unsigned quirks,
                                                     double lr0) {
+  // threads 0..127: Q_target(s) of row b (waves 0-1); threads 128..255: Q_target(s2) of
+  // row b - 128 (waves 2-3) -- the two forwards of a row run side by side
+  __shared__ __attribute__((aligned(16))) float sw[NET_LDS];
+  __shared__ float q[MAX_BATCH][3];
+  __shared__ float val[MAX_BATCH];
+  __shared__ uint32_t sb[MAX_BATCH];
+  __shared__ uint8_t am[MAX_BATCH];
+  __shared__ double part[2];
+  __shared__ int lastw[2][3];
   const TargetJob J = jobs ? jobs[blockIdx.y] : one;
-  const int64_t bx = blockIdx.x;
-#include "br_targets_body.inc"
-}
-
-// one update's targets by the calling workgroup (the persistent group BR kernel's helpers)
-__device__ __forceinline__ void br_targets_item(const TargetJob J, int64_t bx, int B, int E, double gamma,
-                                                unsigned quirks, double lr0) {
-#include "br_targets_body.inc"
-}
-
-// ---------------------------------------------------------------------------
-// k_br_persist: an engine group's whole BR learner call in one launch (round 5).  Workgroups
-// 0 .. njobs - 1 are chains, one per (replica, agent) with BR work: each runs its target-sync
-// segments in order, in pieces of `chunk` updates, each piece as soon as the helpers have
-// written its records.  The other workgroups are helpers: they take work items -- (segment,
-// update) -- in queue order and write that update's targets and step records (k_br_targets'
-// body).  The first segments' items are queued by the host; a chain queues the items of its
-// next segment once the segment's last piece has synced the target net they read.  No
-// round waits for another job's segment, and no targets launch sits between chains (the
-// round structure of the other path: DESIGN.md §4.5).  The same SGD steps as the rounds, bit
-// for bit.
-// Cross-workgroup hand-offs, agent scope (MI355X: per-XCD L2s): the writer's stores, then
-// __threadfence in every writing thread, the workgroup barrier and one release atomic; the
-// reader's relaxed polls in one thread, one acquire fence, then the workgroup barrier (an
-// acquire per poll invalidates the caches every time: the first build crawled).  Every wait is bounded
-// (BRP_SPIN): on expiry the kernel sets *err and the workgroup leaves, so a broken hand-off
-// ends the kernel instead of hanging it (the host reports *err after the step).
-// ---------------------------------------------------------------------------
-struct BrPersistArgs {
-  ChainArgs C;                  // B, E (the chains' jobs come from seg_job)
-  const ChainJob* seg_job;      // [nseg] chain job of each segment (u0, u1: the segment; sync_to)
-  const TargetJob* seg_tgt;     // [nseg] its targets job
-  const int32_t* seg_chunk0;    // [nseg] its first chunk counter
-  const int32_t* job_seg0;      // [njobs + 1] the segments of chain workgroup j: [job_seg0[j], job_seg0[j + 1])
-  uint32_t* slots;              // [nitems] work items (segment << 16 | update in it); BRP_EMPTY until queued
-  uint32_t* ctr;                // [0] helpers' claims, [1] queue reservations
-  uint32_t* chunk_done;         // finished items per chunk
-  int32_t* err;
-  int njobs, nitems, chunk;
-  int spin;                     // bound of every wait (s_sleep 8 rounds)
-  double gamma, lr0;
-  unsigned quirks;
-};
-constexpr uint32_t BRP_EMPTY = 0xFFFFFFFFu, BRP_DONE = 0xFFFFFFFEu;
-constexpr int BRP_SPIN = 1 << 18;   // x s_sleep 8 (~0.1 s; NFSP_BRP_SPIN): well past any legitimate wait
-
-constexpr int BRP_CHUNK = 16;     // updates per chain piece (readiness is checked per piece)
-constexpr int BRP_HELPERS = 48;   // helper workgroups
-constexpr int BRP_STATIC_LDS = 16 * 1024;   // bound on the kernel's static LDS (the targets buffers)
-
-__global__ void __launch_bounds__(256) k_br_persist(BrPersistArgs P);
-
-// launch with a CU per workgroup: dynamic LDS up to what the CU has left beside the kernel's
-// static LDS (the helpers' targets buffers), as the one-engine chains reserve theirs
-static int launch_br_persist(const BrPersistArgs& P, int helpers, hipStream_t s) {
-  static std::atomic<uint64_t> mask{0};
-  static std::atomic<int> dyn{0};
-  int dev = 0;
-  NFSP_HIP(hipGetDevice(&dev));
-  const uint64_t bit = 1ull << (dev & 63);
-  if (!(mask.load(std::memory_order_acquire) & bit)) {
-    // static + dynamic LDS = CHAIN_LDS, what a one-engine chain workgroup takes: a workgroup
-    // asking for more than a CU holds would never be dispatched
-    hipFuncAttributes fa{};
-    NFSP_HIP(hipFuncGetAttributes(&fa, (const void*)k_br_persist));
-    if ((int)fa.sharedSizeBytes > BRP_STATIC_LDS) return nfsp::fail(NFSP_EINVAL, "k_br_persist: static LDS");
-    const int d = CHAIN_LDS - BRP_STATIC_LDS;
-    if (d < (int)sizeof(Chain3Smem)) return nfsp::fail(NFSP_EINVAL, "k_br_persist: LDS");
-    NFSP_HIP(hipFuncSetAttribute((const void*)k_br_persist, hipFuncAttributeMaxDynamicSharedMemorySize, d));
-    dyn.store(d, std::memory_order_release);
-    mask.fetch_or(bit, std::memory_order_acq_rel);
+  if ((int64_t)blockIdx.x >= J.n) return;            // block-uniform
+  const int tid = threadIdx.x;
+  const int b = tid & (MAX_BATCH - 1);
+  const bool s2half = tid >= MAX_BATCH;
+  const int64_t u = J.u0 + blockIdx.x;
+  BrRow rr{};
+  if (b < B) rr = J.rows[u * B + b];
+  // the records of epoch e are emitted by threads 128 (e & 1) .. + 127 (below); their fit
+  // order is loaded now, beside the net
+  const int half = tid >> 7;
+  int pk[2] = {0, 0};
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int e = half + 2 * k;
+    if (e < E && b < B) pk[k] = J.perm[(u * E + e) * B + b];
   }
-  k_br_persist<<<P.njobs + helpers, 256, dyn.load(std::memory_order_acquire), s>>>(P);
-  NFSP_LAUNCHED("k_br_persist");
-  return NFSP_OK;
-}
-
-__global__ void __launch_bounds__(256) k_br_persist(BrPersistArgs P) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  __shared__ uint32_t s_word;
-  if ((int)blockIdx.x < P.njobs) {                         // ---- a chain
-    const int j = blockIdx.x;
-    for (int s = P.job_seg0[j]; s < P.job_seg0[j + 1]; ++s) {
-      const ChainJob JS = P.seg_job[s];
-      for (int64_t a = JS.u0, c = 0; a < JS.u1; a += P.chunk, ++c) {
-        const int64_t b = a + P.chunk < JS.u1 ? a + P.chunk : JS.u1;
-        if (threadIdx.x == 0) {
-          uint32_t* const done = &P.chunk_done[P.seg_chunk0[s] + c];
-          int it = 0;
-          // poll relaxed (an acquire per poll would invalidate the caches every time), then one
-          // acquire fence once the count is reached
-          while (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)(b - a) &&
-                 ++it < P.spin)
-            __builtin_amdgcn_s_sleep(8);
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          s_word = it >= P.spin;
-          if (s_word) {
-            __hip_atomic_store(P.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_fetch_add(&P.err[2], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-        }
-        __syncthreads();
-        if (s_word) return;                                 // workgroup-uniform
-        ChainJob JP = JS;
-        JP.u0 = a;
-        JP.u1 = b;
-        if (b < JS.u1) JP.sync_to = nullptr;                // the segment's last piece syncs
-        chain3_run<1, 0, 1>(P.C, JP, smem_raw);
-        __threadfence();        // the piece's weights (and synced target net) out, for the next
-        __syncthreads();        // piece's loads by other waves and for the helpers
-        if (threadIdx.x == 0) __hip_atomic_fetch_add(&P.err[4], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      if (s + 1 < P.job_seg0[j + 1]) {                      // queue the next segment's items
-        const uint32_t m = (uint32_t)P.seg_tgt[s + 1].n;
-        if (threadIdx.x == 0) s_word = __hip_atomic_fetch_add(&P.ctr[1], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();
-        const uint32_t base = s_word;
-        for (uint32_t i = threadIdx.x; i < m; i += blockDim.x)
-          __hip_atomic_store(&P.slots[base + i], ((uint32_t)(s + 1) << 16) | i, __ATOMIC_RELEASE,
-                             __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();        // s_word is rewritten by the next wait
-      }
+  stage_net_lds(sw, J.tw, tid, blockDim.x);
+  __syncthreads();
+  if (b < B) {
+    float y[3];
+    if (!s2half) {
+      fwd_lds(sw, rr.s, br_act(quirks), y);
+      q[b][0] = y[0]; q[b][1] = y[1]; q[b][2] = y[2];
+      am[b] = (uint8_t)(rr.meta & 0xFFu);
+      sb[b] = rr.s;
+    } else {
+      fwd_lds(sw, rr.s2, br_act(quirks), y);
+      const float qmax = fmaxf(fmaxf(y[0], y[1]), y[2]);
+      const float r = (float)(int8_t)((rr.meta >> 16) & 0xFFu) * 0.5f;
+      const bool terminal = !(quirks & NFSP_QUIRK_TERMINAL_BOOTSTRAP) && ((rr.meta >> 8) & 1u);
+      val[b] = (float)(terminal ? (double)r : (double)r + gamma * (double)qmax);
     }
-    return;
   }
-  for (;;) {                                                // ---- a helper
-    if (threadIdx.x == 0) {
-      const uint32_t p = __hip_atomic_fetch_add(&P.ctr[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      uint32_t v = BRP_DONE;
-      if (p < (uint32_t)P.nitems) {
-        int it = 0;
-        while ((v = __hip_atomic_load(&P.slots[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == BRP_EMPTY &&
-               ++it < P.spin)
-          __builtin_amdgcn_s_sleep(8);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        if (v == BRP_EMPTY) {
-          __hip_atomic_store(P.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_fetch_add(&P.err[3], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          v = BRP_DONE;
-        }
-      }
-      s_word = v;
+  __syncthreads();
+  const int lane = tid & 63, wv = tid >> 6;
+  if (!s2half) {
+    // exploitability proxy (agent/agent.py:235-238): mean of the row maxima, before the
+    // row-0 overwrite; and for the quirk, the last row k with argmax a_k == action
+    double m = b < B ? (double)fmaxf(fmaxf(q[b][0], q[b][1]), q[b][2]) : 0.0;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) m += __shfl_xor(m, off);
+    if (lane == 0) part[wv] = m;
+#pragma unroll
+    for (int act = 0; act < 3; ++act) {
+      const unsigned long long bal = __ballot(b < B && am[b] == act);
+      if (lane == 0) lastw[wv][act] = bal ? 64 * wv + 63 - __builtin_clzll(bal) : -1;
     }
-    __syncthreads();
-    const uint32_t v = s_word;
-    __syncthreads();
-    if (v == BRP_DONE) return;                              // workgroup-uniform
-    const int s = (int)(v >> 16);
-    const int64_t i = (int64_t)(v & 0xFFFFu);
-    br_targets_item(P.seg_tgt[s], i, P.C.B, P.C.E, P.gamma, P.quirks, P.lr0);
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __hip_atomic_fetch_add(&P.chunk_done[P.seg_chunk0[s] + i / P.chunk], 1u, __ATOMIC_RELEASE,
-                             __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_fetch_add(&P.err[5], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (tid == 0) J.expl[u] = (part[0] + part[1]) / B;
+  if (quirks & NFSP_QUIRK_ROW0_TARGET) {
+    if (tid < 3) {       // target[0][argmax a_k] = v_k for k = 0..B-1: the last k wins
+      const int last = lastw[1][tid] >= 0 ? lastw[1][tid] : lastw[0][tid];
+      if (last >= 0) q[0][tid] = val[last];
     }
+  } else if (!s2half && b < B) {
+    q[b][am[b]] = val[b];
+  }
+  __syncthreads();
+  // lr of this update: lr0 / (1 + 0.003 sqrt(iteration)) with iteration = it0 + 2 u
+  // (agent/agent.py:249, iteration += 2 per BR update), in the reference's double arithmetic
+  const float lr = (float)(lr0 / (1.0 + 0.003 * sqrt((double)(J.it0 + 2 * u))));
+  // epochs in pairs: threads 0..127 emit epoch e, threads 128..255 epoch e + 1
+  for (int e = half, k = 0; e < E; e += 2, ++k) {
+    uint32_t x = 0;
+    float t0 = 0.f, t1 = 0.f, t2 = 0.f;
+    if (b < B) {
+      const int r = k < 2 ? pk[k] : J.perm[(u * E + e) * B + b];
+      x = sb[r];
+      t0 = q[r][0]; t1 = q[r][1]; t2 = q[r][2];
+    }
+    emit_recs(J.rec + (u * E + e) * (B / CHAIN_MB), x, t0, t1, t2, lr, B, b);
   }
 }
 
@@ -983,7 +905,6 @@ struct nfsp_group {
   char* d_tab[2] = {nullptr, nullptr};
   size_t tab_cap[2] = {0, 0};
   hipEvent_t snap_ev[2][2] = {};  // pipelined step: [parity][AR, BR stream] snapshot copies done
-  int32_t* d_err = nullptr;       // k_br_persist: a bounded wait expired (checked after each step)
   // the replicas' EngineDev, gathered on device and read back in one copy
   EngineDev** d_stp = nullptr;   // [R] -> each replica's state
   EngineDev* d_st = nullptr;     // [R]
@@ -1025,7 +946,7 @@ extern "C" int nfsp_group_destroy(nfsp_group* g) {
       if (ev) (void)hipEventDestroy(ev);
   }
   if (g->h_st) (void)hipHostFree(g->h_st);
-  for (void* p : {(void*)g->d_err, (void*)g->d_war, (void*)g->w0, g->d_roll, (void*)g->d_stp, (void*)g->d_st})
+  for (void* p : {(void*)g->d_war, (void*)g->w0, g->d_roll, (void*)g->d_stp, (void*)g->d_st})
     if (p) (void)hipFree(p);
   for (hipStream_t st : {g->s_ar, g->s_br})
     if (st) (void)hipStreamDestroy(st);
@@ -1095,8 +1016,6 @@ extern "C" int nfsp_group_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, int 
   }
   hipError_t r = hipMalloc((void**)&g->d_war, sizeof(float*) * war.size());
   if (r == hipSuccess) r = hipMalloc((void**)&g->w0, sizeof(float) * 3 * 2 * nn::NP);
-  if (r == hipSuccess) r = hipMalloc((void**)&g->d_err, sizeof(int32_t) * 8);
-  if (r == hipSuccess) r = hipMemset(g->d_err, 0, sizeof(int32_t) * 8);
   if (r == hipSuccess) r = hipMemcpy(g->d_war, war.data(), sizeof(float*) * war.size(), hipMemcpyHostToDevice);
   if (r == hipSuccess) r = hipMalloc((void**)&g->d_stp, sizeof(EngineDev*) * replicas);
   if (r == hipSuccess) r = hipMalloc((void**)&g->d_st, sizeof(EngineDev) * replicas);
@@ -1255,55 +1174,10 @@ static int group_update(nfsp_group* g, bool pipelined = false, int par = 0, bool
   br_off.push_back(br_jobs.size());
   tg_off.push_back(tg_jobs.size());
   g->rounds = (int64_t)rounds;
-  // The persistent BR kernel (k_br_persist) instead of the rounds: groups of up to 32 replicas
-  // (its 2R chain and BRP_HELPERS helper workgroups, a CU each, beside the 2R AR chains),
-  // the reference's BR net (not the linear-Q extension), no loss log; NFSP_GROUP_BR_PERSIST=0
-  // keeps the rounds.  Its tables: each segment's chain and targets jobs, chunk counters, and
-  // the work queue with the first segments' items, chunk by chunk across the jobs.
-  static const int persist_env = getenv("NFSP_GROUP_BR_PERSIST") ? atoi(getenv("NFSP_GROUP_BR_PERSIST")) : 0;
-  const bool persist = persist_env != 0 && !loss_log && !(cfg.quirks & NFSP_EXT_LINEAR_Q) && R <= 32 &&
-                       !br_jobs.empty();
-  std::vector<ChainJob> p_job;
-  std::vector<TargetJob> p_tgt;
-  std::vector<int32_t> p_chunk0, p_jseg0;
-  std::vector<uint32_t> p_slots;
-  int32_t p_nchunks = 0;
-  uint32_t p_npre = 0;
-  if (persist) {
-    for (int r = 0; r < R; ++r)
-      for (int a = 0; a < 2; ++a) {
-        if (L[r].seg[a].empty()) continue;
-        p_jseg0.push_back((int32_t)p_job.size());
-        for (const Segment& sg : L[r].seg[a]) {
-          NFSP_REQUIRE(sg.v - sg.u < 65536, "a BR segment of >= 65536 updates");
-          p_job.push_back(br_chain_job(g->eng[r], a, sg));
-          p_tgt.push_back(br_target_job(g->eng[r], L[r], a, sg));
-          p_chunk0.push_back(p_nchunks);
-          p_nchunks += (int32_t)((sg.v - sg.u + BRP_CHUNK - 1) / BRP_CHUNK);
-        }
-      }
-    NFSP_REQUIRE(p_job.size() < 65536, "too many BR segments in one learner call");
-    const int njobs = (int)p_jseg0.size();
-    p_jseg0.push_back((int32_t)p_job.size());
-    int64_t nitems = 0, maxn = 0;
-    for (const TargetJob& t : p_tgt) nitems += t.n;
-    for (int j = 0; j < njobs; ++j) maxn = p_tgt[p_jseg0[j]].n > maxn ? p_tgt[p_jseg0[j]].n : maxn;
-    p_slots.assign((size_t)nitems, BRP_EMPTY);
-    for (int64_t c0 = 0; c0 < maxn; c0 += BRP_CHUNK)
-      for (int j = 0; j < njobs; ++j) {
-        const int sgi = p_jseg0[j];
-        const int64_t n = p_tgt[sgi].n, c1 = c0 + BRP_CHUNK < n ? c0 + BRP_CHUNK : n;
-        for (int64_t i = c0; i < c1; ++i) p_slots[p_npre++] = ((uint32_t)sgi << 16) | (uint32_t)i;
-      }
-  }
   TabCursor cur;
   const size_t o_prep = cur.take<PrepArgs>(R), o_fin = cur.take<FinalArgs>(R);
   const size_t o_ar = cur.take<ChainJob>(ar_jobs.size()), o_br = cur.take<ChainJob>(br_jobs.size());
   const size_t o_tg = cur.take<TargetJob>(tg_jobs.size());
-  const size_t o_pj = cur.take<ChainJob>(p_job.size()), o_pt = cur.take<TargetJob>(p_tgt.size());
-  const size_t o_pc = cur.take<int32_t>(p_chunk0.size()), o_ps = cur.take<int32_t>(p_jseg0.size());
-  const size_t o_pq = cur.take<uint32_t>(p_slots.size()), o_pn = cur.take<uint32_t>(2);
-  const size_t o_pd = cur.take<uint32_t>((size_t)p_nchunks);
   const size_t need = cur.off;
   // Every earlier use of set `par` has completed: serially, the call starts with the readback's
   // sync; pipelined, the ctx stream waited for slice j - 2's snapshot events (after its chains)
@@ -1329,16 +1203,6 @@ static int group_update(nfsp_group* g, bool pipelined = false, int par = 0, bool
   memcpy(h_tab + o_ar, ar_jobs.data(), sizeof(ChainJob) * ar_jobs.size());
   memcpy(h_tab + o_br, br_jobs.data(), sizeof(ChainJob) * br_jobs.size());
   memcpy(h_tab + o_tg, tg_jobs.data(), sizeof(TargetJob) * tg_jobs.size());
-  if (persist) {
-    memcpy(h_tab + o_pj, p_job.data(), sizeof(ChainJob) * p_job.size());
-    memcpy(h_tab + o_pt, p_tgt.data(), sizeof(TargetJob) * p_tgt.size());
-    memcpy(h_tab + o_pc, p_chunk0.data(), sizeof(int32_t) * p_chunk0.size());
-    memcpy(h_tab + o_ps, p_jseg0.data(), sizeof(int32_t) * p_jseg0.size());
-    memcpy(h_tab + o_pq, p_slots.data(), sizeof(uint32_t) * p_slots.size());
-    const uint32_t ctr[2] = {0u, p_npre};
-    memcpy(h_tab + o_pn, ctr, sizeof(ctr));
-    memset(h_tab + o_pd, 0, sizeof(uint32_t) * (size_t)p_nchunks);
-  }
   const PrepArgs* d_prep = reinterpret_cast<const PrepArgs*>(d_tab + o_prep);
   const FinalArgs* d_fin = reinterpret_cast<const FinalArgs*>(d_tab + o_fin);
   const ChainJob* d_ar = reinterpret_cast<const ChainJob*>(d_tab + o_ar);
@@ -1404,34 +1268,7 @@ static int group_update(nfsp_group* g, bool pipelined = false, int par = 0, bool
   }
   NFSP_HIP(hipStreamWaitEvent(g->s_br, fork_br, 0));
   KTimer kspan(e0, KT_BR_STREAM0, g->s_br);     // the group's one BR stream, end to end
-  if (persist) {
-    if (!ar_launched) {
-      if ((rc = launch_ar(nullptr)) != NFSP_OK) return rc;
-      ar_launched = true;
-    }
-    BrPersistArgs P{};
-    P.C.B = cfg.batch;
-    P.C.E = cfg.epochs;
-    P.seg_job = reinterpret_cast<const ChainJob*>(d_tab + o_pj);
-    P.seg_tgt = reinterpret_cast<const TargetJob*>(d_tab + o_pt);
-    P.seg_chunk0 = reinterpret_cast<const int32_t*>(d_tab + o_pc);
-    P.job_seg0 = reinterpret_cast<const int32_t*>(d_tab + o_ps);
-    P.slots = reinterpret_cast<uint32_t*>(d_tab + o_pq);
-    P.ctr = reinterpret_cast<uint32_t*>(d_tab + o_pn);
-    P.chunk_done = reinterpret_cast<uint32_t*>(d_tab + o_pd);
-    P.err = g->d_err;
-    P.njobs = (int)p_jseg0.size() - 1;
-    P.nitems = (int)p_slots.size();
-    P.chunk = BRP_CHUNK;
-    P.gamma = cfg.gamma;
-    P.lr0 = cfg.lr_br;
-    P.quirks = cfg.quirks;
-    static const int spin_env = getenv("NFSP_BRP_SPIN") ? atoi(getenv("NFSP_BRP_SPIN")) : BRP_SPIN;
-    P.spin = spin_env;
-    KTimer kc(e0, KT_CHAIN_BR, g->s_br);
-    if ((rc = launch_br_persist(P, BRP_HELPERS, g->s_br)) != NFSP_OK) return rc;
-  }
-  for (size_t k = 0; k < (persist ? 0 : rounds); ++k) {
+  for (size_t k = 0; k < rounds; ++k) {
     const int nj = (int)(br_off[k + 1] - br_off[k]);
     const int nt = (int)(tg_off[k + 1] - tg_off[k]);
     if (nt > 0) {
@@ -1536,7 +1373,7 @@ extern "C" int nfsp_group_get_timings(nfsp_group* g, double* ms, int64_t* launch
 // slices run one after another, but slice j acts with snapshot j & 1: the nets and epsilon as
 // slice j - 2's learner (and exchange) left them, the step's start for j < 2 -- a pipelined
 // engine's arithmetic (step_pipelined).
-static int group_step_impl(nfsp_group* g) {
+extern "C" int nfsp_group_step(nfsp_group* g) {
   NFSP_REQUIRE(g, "null argument");
   int rc;
   if (g->xchg_nets & ~g->w0_valid)      // common nets before the first exchange
@@ -1577,29 +1414,6 @@ static int group_step_impl(nfsp_group* g) {
       return rc;
   }
   return NFSP_OK;
-}
-
-// k_br_persist's bounded waits: a hand-off that never came ends the kernel with *err set
-static int group_check_err(nfsp_group* g) {
-  int32_t h[8] = {};
-  NFSP_HIP(hipMemcpyAsync(h, g->d_err, sizeof(h), hipMemcpyDeviceToHost, g->ctx->stream));
-  NFSP_HIP(hipStreamSynchronize(g->ctx->stream));
-  static const bool dbg = getenv("NFSP_BRP_DEBUG") && atoi(getenv("NFSP_BRP_DEBUG"));
-  if (dbg) fprintf(stderr, "k_br_persist: err %d, chain bails %d, helper bails %d, pieces %d, items %d\n",
-                   h[0], h[2], h[3], h[4], h[5]);
-  if (h[0] || dbg) NFSP_HIP(hipMemset(g->d_err, 0, sizeof(h)));
-  if (h[0])
-    return nfsp::fail(NFSP_EHIP, "k_br_persist: a bounded wait expired (work-queue hand-off): chain bails " +
-                                     std::to_string(h[2]) + ", helper bails " + std::to_string(h[3]) + ", pieces " +
-                                     std::to_string(h[4]) + ", items " + std::to_string(h[5]));
-  return NFSP_OK;
-}
-
-extern "C" int nfsp_group_step(nfsp_group* g) {
-  NFSP_REQUIRE(g, "null argument");
-  const int rc = group_step_impl(g);
-  if (rc != NFSP_OK) return rc;
-  return group_check_err(g);
 }
 
 extern "C" int nfsp_group_rounds(nfsp_group* g, int64_t* out) {
