@@ -12,7 +12,8 @@ __all__ = ["native", "install_dropin"]
 def __getattr__(name):
     # heavy submodules (torch) load lazily so `native` can be probed without a GPU stack
     import importlib
-    if name in ("leduc", "agent", "buffers", "selfplay", "engine", "observability", "pyrandom", "shards"):
+    if name in ("leduc", "agent", "buffers", "selfplay", "engine", "observability", "pyrandom", "shards",
+                "reference_main"):
         return importlib.import_module(f".{name}", __name__)
     raise AttributeError(name)
 

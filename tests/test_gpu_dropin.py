@@ -125,3 +125,56 @@ def test_dropin_main_train_matches_oracle(pkg):
         for m in ("avg_strategy_model", "best_response_model", "target_br_model"):
             for x, y in zip(getattr(a, m).get_weights(), getattr(b, m).get_weights()):
                 assert np.abs(x - y).max() <= 1e-4, m
+
+
+# A driver with main.py's module-level imports and main() (main.py:1-18,127-146), written
+# for this test (the reference checkout is not on the GPU box): `reference_main.run`
+# resolves its imports to the drop-in and the stand-ins, runs it as __main__ in its own
+# directory, and it trains on the GPU classes.  tests/test_reference_main.py runs the
+# reference's own main.py through the same launcher on CPU.
+_DRIVER = '''
+import random
+import tensorflow as tf
+import leduc.newenv as leduc
+import agent.agent as agent
+import numpy as np
+import ConfigParser
+import matplotlib.pyplot as plt
+
+Config = ConfigParser.ConfigParser()
+Config.read("./config.ini")
+
+if __name__ == "__main__":
+    import nfsp_amd
+    with tf.Session() as sess:
+        env = leduc.Env()
+        np.random.seed(int(Config.get("Utils", "Seed")))
+        tf.set_random_seed(int(Config.get("Utils", "Seed")))
+        p1 = agent.Agent(sess, env.observation_space, env.action_space, "Player0", env)
+        p2 = agent.Agent(sess, env.observation_space, env.action_space, "Player1", env)
+        sess.run(tf.global_variables_initializer())
+        assert type(env) is nfsp_amd.leduc.Env and type(p1) is nfsp_amd.agent.Agent
+        curve = nfsp_amd.selfplay.train(env, p1, p2, episodes=int(Config.get("Common", "Episodes")),
+                                        eta=float(Config.get("Agent", "Eta")))
+        plt.plot(curve)
+        plt.show()
+'''
+
+
+def test_reference_main_launcher_runs_a_driver_on_the_gpu_dropin(pkg, tmp_path):
+    (tmp_path / "main.py").write_text(_DRIVER)
+    (tmp_path / "config.ini").write_text("[Agent]\nEta: 0.1\n[Utils]\nSeed: 1234\n[Common]\nEpisodes: 400000\n")
+    episodes = 450
+    random.seed(99)
+    out = pkg.reference_main.run(str(tmp_path / "main.py"), episodes=episodes, plot_to=str(tmp_path / "curve"))
+    assert out["tf_seeds"] == [1234]
+    curve = out["curves"][0]
+    assert len(curve) == len([i for i in range(episodes) if i > 150 and i % 100 == 0])
+    assert (tmp_path / "curve.csv").exists()
+    # the same run without the launcher, from the same seeds: identical (one deterministic path)
+    random.seed(99)
+    env = pkg.leduc.Env()
+    np.random.seed(1234)
+    p1 = pkg.agent.Agent(None, env.observation_space, env.action_space, "Player0", env)
+    p2 = pkg.agent.Agent(None, env.observation_space, env.action_space, "Player1", env)
+    assert curve == pkg.selfplay.train(env, p1, p2, episodes=episodes)

@@ -1,0 +1,79 @@
+"""The reference's own main.py, unchanged, through nfsp_amd.reference_main (CPU).
+
+`reference_main.run` supplies the host-side modules main.py imports besides the drop-in
+(tensorflow, matplotlib.pyplot, ConfigParser) and runs the file as __main__ in its own
+directory.  Here, without a GPU, the leduc.newenv / agent.agent registrations are the CPU
+oracle's classes (test infrastructure); the GPU suite runs the same launcher on the drop-in
+(tests/test_gpu_dropin.py).  The run must be main.train's: the same curve, hand for hand,
+as the oracle's restatement of main.train (nfsp_oracle.train, pinned to the reference's
+event log) from the same seeds.
+"""
+import os
+import random
+import types
+
+import numpy as np
+import pytest
+
+import nfsp_oracle as orc
+
+REF_MAIN = "/root/reference/main.py"
+
+
+def _oracle_modules():
+    leduc = types.ModuleType("leduc")
+    leduc.__path__ = []
+    newenv = types.ModuleType("leduc.newenv")
+    newenv.Env = orc.Env
+    leduc.newenv = newenv
+    agent = types.ModuleType("agent")
+    agent.__path__ = []
+    agentm = types.ModuleType("agent.agent")
+    agentm.Agent = orc.Agent
+    agent.agent = agentm
+    return {"leduc": leduc, "leduc.newenv": newenv, "agent": agent, "agent.agent": agentm}
+
+
+def test_stubs_cover_what_main_py_uses(pkg):
+    rm = pkg.reference_main
+    tf = rm.tensorflow_stub()
+    with tf.Session() as sess:
+        assert sess.run(tf.global_variables_initializer()) is None
+    assert sess.closed
+    tf.set_random_seed(1234)
+    assert tf.seeds == [1234]
+    mpl, plt = rm.matplotlib_stub()
+    plt.plot([1.0, 2.0])
+    plt.show()
+    assert plt.curves == [[1.0, 2.0]] and mpl.pyplot is plt
+    cp = rm.configparser_stub({("Common", "Episodes"): 7}).ConfigParser()
+    cp.read_string("[Common]\nEpisodes: 400000\n[Agent]\nEta: 0.1\n")
+    assert cp.get("Common", "Episodes") == "7" and cp.get("Agent", "Eta") == "0.1"
+
+
+@pytest.mark.skipif(not os.path.isfile(REF_MAIN), reason="the reference checkout is not present")
+def test_reference_main_py_runs_unchanged(pkg, capsys):
+    before = open(REF_MAIN, "rb").read()
+    episodes = 450
+    random.seed(20261017)
+    out = pkg.reference_main.run(REF_MAIN, episodes=episodes, modules=_oracle_modules())
+    assert open(REF_MAIN, "rb").read() == before              # nothing edited
+    printed = capsys.readouterr().out
+    assert "NFSP by David Joos" in printed                    # main.py:151, its __main__ block ran
+    assert out["tf_seeds"] == [1234]                          # main.py:133 with config.ini's Seed
+    reports = [i for i in range(episodes) if i > 150 and i % 100 == 0]
+    assert printed.count("Exploitability:") == len(reports)
+    assert out["curves"] is not None and len(out["curves"]) == 1
+    curve = out["curves"][0]
+    assert len(curve) == len(reports)
+
+    # the oracle's main.train from the same state: main.main() is Env(), np.random.seed(Seed),
+    # two Agents, train (main.py:127-146); the stdlib `random` main.py draws from is unseeded
+    # by it, so both runs start from random.seed(20261017)
+    random.seed(20261017)
+    env = orc.Env()
+    np.random.seed(1234)
+    p1 = orc.Agent(None, env.observation_space, env.action_space, "Player0", env)
+    p2 = orc.Agent(None, env.observation_space, env.action_space, "Player1", env)
+    ref = orc.train(env, p1, p2, episodes)
+    assert curve == ref
