@@ -14,8 +14,8 @@ that do what main.py asks of them and nothing else:
   Agent keeps its nets on the GPU and ignores the session, as the reference's Keras models
   bind to the default one.
 * ``matplotlib`` / ``matplotlib.pyplot``: ``plot`` keeps the curve (``run`` returns it);
-  ``show`` does nothing, or writes the curve to ``plot_to``.csv / .png
-  (``observability.save_curve``) when a path is given: main.py would open a window.
+  ``show`` opens no window; with ``plot_to``, the shown curve is written to
+  ``plot_to``.csv / .png (``observability.save_curve``) once the file has run.
 * ``ConfigParser``: Python 3's ``configparser.ConfigParser``, optionally with overrides
   (e.g. ``Common.Episodes`` for a short run).
 
@@ -73,17 +73,16 @@ def tensorflow_stub() -> types.ModuleType:
     return tf
 
 
-def matplotlib_stub(plot_to: str | None = None):
+def matplotlib_stub():
     mpl = types.ModuleType("matplotlib")
     plt = types.ModuleType("matplotlib.pyplot")
     mpl.__nfsp_stub__ = plt.__nfsp_stub__ = True
     plt.curves = []
+    plt.shown = 0
     plt.plot = lambda y, *a, **k: plt.curves.append(list(y))
 
     def show(*a, **k):
-        if plot_to and plt.curves:
-            from .observability import save_curve
-            save_curve(plt.curves[-1], plot_to + ".csv", plot_to + ".png", xlabel="report")
+        plt.shown += 1
 
     plt.show = show
     mpl.pyplot = plt
@@ -143,7 +142,7 @@ def run(main_py: str, episodes: int | None = None, argv=(), overrides: dict | No
     episodes: overrides ``[Common] Episodes`` of its config.ini (main.py:27);
     overrides: further ``{(section, option): value}`` for its ConfigParser;
     skip_sleep: the ``time.sleep(60)`` after ``plt.show()`` (main.py:124) returns at once;
-    plot_to: ``plt.show()`` writes the curve to <plot_to>.csv / .png;
+    plot_to: the curve ``plt.show()`` was asked to show goes to <plot_to>.csv / .png;
     modules: replaces the drop-in's module registrations (tests: the CPU oracle's classes).
     Returns ``{"globals": the module's globals, "curves": what it passed to plt.plot,
     "tf_seeds": its tf.set_random_seed calls}``."""
@@ -161,11 +160,14 @@ def run(main_py: str, episodes: int | None = None, argv=(), overrides: dict | No
         mods = dict(modules)
     tf = tensorflow_stub()
     mods["tensorflow"] = tf
-    mpl, plt = matplotlib_stub(plot_to)
+    mpl, plt = matplotlib_stub()
     mods["matplotlib"], mods["matplotlib.pyplot"] = mpl, plt
     mods["ConfigParser"] = configparser_stub(ov)
     with _patched(mods, [main_py, *argv], os.path.dirname(main_py), skip_sleep):
         g = runpy.run_path(main_py, run_name="__main__")
+    if plot_to and plt.shown and plt.curves:       # after the stand-ins are gone (real pyplot)
+        from .observability import save_curve
+        save_curve(plt.curves[-1], plot_to + ".csv", plot_to + ".png", xlabel="report")
     return {"globals": g, "curves": plt.curves, "tf_seeds": tf.seeds}
 
 

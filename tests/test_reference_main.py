@@ -45,18 +45,19 @@ def test_stubs_cover_what_main_py_uses(pkg):
     mpl, plt = rm.matplotlib_stub()
     plt.plot([1.0, 2.0])
     plt.show()
-    assert plt.curves == [[1.0, 2.0]] and mpl.pyplot is plt
+    assert plt.curves == [[1.0, 2.0]] and plt.shown == 1 and mpl.pyplot is plt
     cp = rm.configparser_stub({("Common", "Episodes"): 7}).ConfigParser()
     cp.read_string("[Common]\nEpisodes: 400000\n[Agent]\nEta: 0.1\n")
     assert cp.get("Common", "Episodes") == "7" and cp.get("Agent", "Eta") == "0.1"
 
 
 @pytest.mark.skipif(not os.path.isfile(REF_MAIN), reason="the reference checkout is not present")
-def test_reference_main_py_runs_unchanged(pkg, capsys):
+def test_reference_main_py_runs_unchanged(pkg, capsys, tmp_path):
     before = open(REF_MAIN, "rb").read()
     episodes = 450
     random.seed(20261017)
-    out = pkg.reference_main.run(REF_MAIN, episodes=episodes, modules=_oracle_modules())
+    out = pkg.reference_main.run(REF_MAIN, episodes=episodes, modules=_oracle_modules(),
+                                 plot_to=str(tmp_path / "curve"))
     assert open(REF_MAIN, "rb").read() == before              # nothing edited
     printed = capsys.readouterr().out
     assert "NFSP by David Joos" in printed                    # main.py:151, its __main__ block ran
@@ -66,6 +67,8 @@ def test_reference_main_py_runs_unchanged(pkg, capsys):
     assert out["curves"] is not None and len(out["curves"]) == 1
     curve = out["curves"][0]
     assert len(curve) == len(reports)
+    rows = (tmp_path / "curve.csv").read_text().strip().split("\n")[1:]   # main.py:122-123's plot
+    assert [float(r.split(",")[1]) for r in rows] == curve
 
     # the oracle's main.train from the same state: main.main() is Env(), np.random.seed(Seed),
     # two Agents, train (main.py:127-146); the stdlib `random` main.py draws from is unseeded
