@@ -795,9 +795,10 @@ int group_rollout_launch(nfsp_engine* const* eng, int R, const void* d_tab, int 
   return NFSP_OK;
 }
 
-int group_snap_part_launch(nfsp_engine* const* eng, int R, const void* d_tab, int par, int part, hipStream_t s) {
-  k_group_snap_part<<<dim3(nfsp_blocks(6 * nn::NP, 256), R), 256, 0, s>>>(static_cast<const GroupRollout*>(d_tab),
-                                                                         par, part);
+int group_snap_part_launch(nfsp_engine* const* eng, int R, const void* d_tab, int par, int part, hipStream_t s,
+                           int r0) {
+  k_group_snap_part<<<dim3(nfsp_blocks(6 * nn::NP, 256), R), 256, 0, s>>>(
+      static_cast<const GroupRollout*>(d_tab) + r0, par, part);
   NFSP_LAUNCHED("k_group_snap_part");
   return NFSP_OK;
 }

@@ -317,7 +317,9 @@ int group_rollout_launch(nfsp_engine* const* eng, int R, const void* d_tab, int 
 // slice_lag 2: every replica's nets and epsilon -> snapshot par (-1: both parities)
 int group_snap_launch(nfsp_engine* const* eng, int R, const void* d_tab, int par);
 // one learner stream's part of it (0: AR nets; 1: BR / target nets and epsilons) on stream s
-int group_snap_part_launch(nfsp_engine* const* eng, int R, const void* d_tab, int par, int part, hipStream_t s);
+// replicas r0 .. r0 + R - 1 of the group's rollout table (eng: from replica r0)
+int group_snap_part_launch(nfsp_engine* const* eng, int R, const void* d_tab, int par, int part, hipStream_t s,
+                           int r0 = 0);
 // the cross-shard exchange of the AR nets, enqueued on `s` (the AR chain stream)
 int exchange_enqueue(nfsp_engine* e, hipStream_t s);
 

@@ -891,12 +891,17 @@ int step_pipelined(nfsp_engine* e) {
 // ---------------------------------------------------------------------------
 // Engine groups (nfsp_group_*): R replicas stepped together, their chains in shared launches
 // ---------------------------------------------------------------------------
+constexpr int GROUP_BR_STREAMS = 4;   // at most; NFSP_GROUP_BR_STREAMS (group_update)
+
 struct nfsp_group {
   nfsp_ctx* ctx = nullptr;
   int R = 0;
   unsigned flags = 0;
   std::vector<nfsp_engine*> eng;
   hipStream_t s_ar = nullptr, s_br = nullptr;
+  // further BR streams: a sliced group's BR jobs run in GROUP_BR_STREAMS partitions, each its
+  // own rounds on its own stream (partition 0 on s_br)
+  hipStream_t s_brp[GROUP_BR_STREAMS - 1] = {};
   void* d_roll = nullptr;        // the replicas' rollout arguments (static device table)
   // per learner call: job / prep / final tables, host (pinned) staging -> device, one copy;
   // two sets by slice parity (a pipelined step's slice j + 1 fills its set while slice j's
@@ -938,6 +943,8 @@ extern "C" int nfsp_group_destroy(nfsp_group* g) {
   if (g->ctx) (void)hipStreamSynchronize(g->ctx->stream);
   for (hipStream_t st : {g->s_ar, g->s_br})
     if (st) (void)hipStreamSynchronize(st);
+  for (hipStream_t st : g->s_brp)
+    if (st) (void)hipStreamSynchronize(st);
   for (nfsp_engine* e : g->eng) nfsp_engine_destroy(e);
   for (int p = 0; p < 2; ++p) {
     if (g->h_tab[p]) (void)hipHostFree(g->h_tab[p]);
@@ -949,6 +956,8 @@ extern "C" int nfsp_group_destroy(nfsp_group* g) {
   for (void* p : {(void*)g->d_war, (void*)g->w0, g->d_roll, (void*)g->d_stp, (void*)g->d_st})
     if (p) (void)hipFree(p);
   for (hipStream_t st : {g->s_ar, g->s_br})
+    if (st) (void)hipStreamDestroy(st);
+  for (hipStream_t st : g->s_brp)
     if (st) (void)hipStreamDestroy(st);
   delete g;
   return NFSP_OK;
@@ -987,7 +996,8 @@ extern "C" int nfsp_group_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, int 
     }
     g->eng.push_back(e);
   }
-  for (hipStream_t* st : {&g->s_ar, &g->s_br}) {
+  static_assert(GROUP_BR_STREAMS == 4, "the streams created below");
+  for (hipStream_t* st : {&g->s_ar, &g->s_br, &g->s_brp[0], &g->s_brp[1], &g->s_brp[2]}) {
     const hipError_t sr = hipStreamCreateWithFlags(st, hipStreamNonBlocking);
     if (sr != hipSuccess) {
       nfsp_group_destroy(g);
@@ -1136,44 +1146,65 @@ static int group_update(nfsp_group* g, bool pipelined = false, int par = 0, bool
   // resume from the weights in memory: the same SGD steps, bit for bit.
   static const int cap_env = getenv("NFSP_GROUP_BR_CAP") ? atoi(getenv("NFSP_GROUP_BR_CAP")) : -1;
   const int64_t cap = cap_env >= 0 ? cap_env : (e0->slices > 1 ? 40 : 0);
+  // Partitions: replicas [pr0[p], pr0[p + 1]) are partition p, whose BR jobs run their own
+  // rounds on their own stream, followed (pipelined) by the partition's BR results and BR
+  // snapshot on that stream.  A round then waits only for the longest piece among its
+  // partition's jobs, one partition's targets overlap the others' chains, and a partition goes
+  // on into the next slice without waiting for the others.  Each job's pieces and targets are
+  // the same as with one partition, so are its SGD steps.  Sliced groups only (their rounds
+  // are short: the targets between them were ~10% of c4_emul_r8's BR stream); groups whose
+  // chains share CUs keep one stream.
+  const bool shared_cus = g->chain_lds < CHAIN_LDS;
+  static const int nbs_env = getenv("NFSP_GROUP_BR_STREAMS") ? atoi(getenv("NFSP_GROUP_BR_STREAMS")) : -1;
+  int nbs = nbs_env > 0 ? nbs_env : (e0->slices > 1 ? 2 : 1);
+  nbs = nbs > GROUP_BR_STREAMS ? GROUP_BR_STREAMS : nbs;
+  nbs = nbs > R ? R : nbs;
+  if (shared_cus) nbs = 1;
   struct BrCursor {
     int r, a;
     size_t s;        // current segment
     int64_t pos;     // next update of it
   };
-  std::vector<BrCursor> bc;
-  for (int r = 0; r < R; ++r)
-    for (int a = 0; a < 2; ++a)
-      if (!L[r].seg[a].empty()) bc.push_back({r, a, 0, L[r].seg[a][0].u});
+  struct BrRound {
+    int p;                   // partition (stream)
+    size_t b0, b1, t0, t1;   // its chain jobs / target jobs in br_jobs / tg_jobs
+    int64_t rn;              // the longest segment starting in it (targets grid)
+  };
   std::vector<ChainJob> br_jobs;
   std::vector<TargetJob> tg_jobs;
-  std::vector<size_t> br_off, tg_off;
-  std::vector<int64_t> round_n;          // the longest starting segment of each round (targets grid)
-  for (;;) {
-    const size_t b0 = br_jobs.size(), t0 = tg_jobs.size();
-    int64_t rn = 0;
-    for (BrCursor& c : bc) {
-      const std::vector<Segment>& segs = L[c.r].seg[c.a];
-      if (c.s >= segs.size()) continue;
-      const Segment& sg = segs[c.s];
-      if (c.pos == sg.u) {
-        tg_jobs.push_back(br_target_job(g->eng[c.r], L[c.r], c.a, sg));
-        rn = sg.v - sg.u > rn ? sg.v - sg.u : rn;
+  std::vector<BrRound> rounds_v;
+  int pr0[GROUP_BR_STREAMS + 1];
+  for (int p = 0; p <= nbs; ++p) pr0[p] = p * R / nbs;
+  int64_t max_rounds = 0;
+  for (int p = 0; p < nbs; ++p) {
+    std::vector<BrCursor> bc;
+    for (int r = pr0[p]; r < pr0[p + 1]; ++r)
+      for (int a = 0; a < 2; ++a)
+        if (!L[r].seg[a].empty()) bc.push_back({r, a, 0, L[r].seg[a][0].u});
+    int64_t nr = 0;
+    for (;;) {
+      const size_t b0 = br_jobs.size(), t0 = tg_jobs.size();
+      int64_t rn = 0;
+      for (BrCursor& c : bc) {
+        const std::vector<Segment>& segs = L[c.r].seg[c.a];
+        if (c.s >= segs.size()) continue;
+        const Segment& sg = segs[c.s];
+        if (c.pos == sg.u) {
+          tg_jobs.push_back(br_target_job(g->eng[c.r], L[c.r], c.a, sg));
+          rn = sg.v - sg.u > rn ? sg.v - sg.u : rn;
+        }
+        const int64_t end = cap > 0 && c.pos + cap < sg.v ? c.pos + cap : sg.v;
+        br_jobs.push_back(br_chain_job(g->eng[c.r], c.a, Segment{c.pos, end, sg.sync && end == sg.v}));
+        c.pos = end;
+        if (end == sg.v && ++c.s < segs.size()) c.pos = segs[c.s].u;
       }
-      const int64_t end = cap > 0 && c.pos + cap < sg.v ? c.pos + cap : sg.v;
-      br_jobs.push_back(br_chain_job(g->eng[c.r], c.a, Segment{c.pos, end, sg.sync && end == sg.v}));
-      c.pos = end;
-      if (end == sg.v && ++c.s < segs.size()) c.pos = segs[c.s].u;
+      if (br_jobs.size() == b0) break;
+      rounds_v.push_back({p, b0, br_jobs.size(), t0, tg_jobs.size(), rn});
+      ++nr;
     }
-    if (br_jobs.size() == b0) break;
-    br_off.push_back(b0);
-    tg_off.push_back(t0);
-    round_n.push_back(rn);
+    max_rounds = nr > max_rounds ? nr : max_rounds;
   }
-  const size_t rounds = round_n.size();
-  br_off.push_back(br_jobs.size());
-  tg_off.push_back(tg_jobs.size());
-  g->rounds = (int64_t)rounds;
+  g->rounds = max_rounds;
   TabCursor cur;
   const size_t o_prep = cur.take<PrepArgs>(R), o_fin = cur.take<FinalArgs>(R);
   const size_t o_ar = cur.take<ChainJob>(ar_jobs.size()), o_br = cur.take<ChainJob>(br_jobs.size());
@@ -1249,7 +1280,6 @@ static int group_update(nfsp_group* g, bool pipelined = false, int par = 0, bool
   // When chains share CUs (R > 64), the first round's BR targets run before the AR chains
   // start: alone they take the chip's issue slots instead of competing with 2R resident AR
   // chains, and the BR stream is the longer one at that size.  (No data dependency.)
-  const bool shared_cus = g->chain_lds < CHAIN_LDS;
   auto launch_ar = [&](hipEvent_t after) -> int {
     NFSP_HIP(hipStreamWaitEvent(g->s_ar, fork, 0));
     if (after) NFSP_HIP(hipStreamWaitEvent(g->s_ar, after, 0));
@@ -1266,48 +1296,63 @@ static int group_update(nfsp_group* g, bool pipelined = false, int par = 0, bool
     if ((rc = launch_ar(nullptr)) != NFSP_OK) return rc;
     ar_launched = true;
   }
-  NFSP_HIP(hipStreamWaitEvent(g->s_br, fork_br, 0));
-  KTimer kspan(e0, KT_BR_STREAM0, g->s_br);     // the group's one BR stream, end to end
-  for (size_t k = 0; k < rounds; ++k) {
-    const int nj = (int)(br_off[k + 1] - br_off[k]);
-    const int nt = (int)(tg_off[k + 1] - tg_off[k]);
+  hipStream_t sp[GROUP_BR_STREAMS] = {g->s_br, g->s_brp[0], g->s_brp[1], g->s_brp[2]};
+  for (int p = 0; p < nbs; ++p) NFSP_HIP(hipStreamWaitEvent(sp[p], fork_br, 0));
+  KTimer kspan(e0, KT_BR_STREAM0, g->s_br);     // the group's BR streams, end to end (joined on s_br)
+  for (const BrRound& rd : rounds_v) {
+    hipStream_t st = sp[rd.p];
+    const int nj = (int)(rd.b1 - rd.b0);
+    const int nt = (int)(rd.t1 - rd.t0);
     if (nt > 0) {
       {
-        KTimer kt2(e0, KT_TARGETS, g->s_br);
-        k_br_targets<<<dim3((unsigned)round_n[k], (unsigned)nt), 256, 0, g->s_br>>>(
-            d_tg + tg_off[k], TargetJob{}, cfg.batch, cfg.epochs, cfg.gamma, cfg.quirks, cfg.lr_br);
+        KTimer kt2(e0, KT_TARGETS, st);
+        k_br_targets<<<dim3((unsigned)rd.rn, (unsigned)nt), 256, 0, st>>>(
+            d_tg + rd.t0, TargetJob{}, cfg.batch, cfg.epochs, cfg.gamma, cfg.quirks, cfg.lr_br);
       }
       NFSP_LAUNCHED("k_br_targets");
     }
-    if (!ar_launched) {
+    if (!ar_launched) {                      // (one partition: shared_cus)
       hipEvent_t t0 = take_event(e0);
-      NFSP_HIP(hipEventRecord(t0, g->s_br));
+      NFSP_HIP(hipEventRecord(t0, st));
       if ((rc = launch_ar(t0)) != NFSP_OK) return rc;
       e0->pool.push_back(t0);
       ar_launched = true;
     }
     ChainArgs C{};
-    C.jobs = d_br + br_off[k];
+    C.jobs = d_br + rd.b0;
     C.B = cfg.batch;
     C.E = cfg.epochs;
     C.lds = g->chain_lds;
-    KTimer kc(e0, KT_CHAIN_BR, g->s_br);
-    if ((rc = launch_br_chain(C, nj, cfg.quirks, loss_log, g->s_br)) != NFSP_OK) return rc;
+    KTimer kc(e0, KT_CHAIN_BR, st);
+    if ((rc = launch_br_chain(C, nj, cfg.quirks, loss_log, st)) != NFSP_OK) return rc;
   }
   if (!ar_launched && (rc = launch_ar(nullptr)) != NFSP_OK) return rc;
+  // each partition's stream: (pipelined) its replicas' BR results, then (snap_after) their BR /
+  // target nets and epsilons into snapshot `par`; then the partitions are joined on s_br
+  for (int p = 0; p < nbs; ++p) {
+    const int r0 = pr0[p], rn = pr0[p + 1] - pr0[p];
+    if (pipelined && rn > 0) {
+      k_finalize<1><<<rn, 64, 0, sp[p]>>>(FinalArgs{}, d_fin + r0, 6);
+      NFSP_LAUNCHED("k_finalize");
+      if (snap_after &&
+          (rc = nfsp::eng::group_snap_part_launch(g->eng.data() + r0, rn, g->d_roll, par, 1, sp[p], r0)) != NFSP_OK)
+        return rc;
+    }
+    if (p > 0) {
+      hipEvent_t j = take_event(e0);
+      NFSP_HIP(hipEventRecord(j, sp[p]));
+      NFSP_HIP(hipStreamWaitEvent(g->s_br, j, 0));
+      e0->pool.push_back(j);
+    }
+  }
   if (pipelined) {
-    // BR stream: the replicas' BR results, then (snap_after) their BR / target nets and
-    // epsilons into snapshot `par`
-    k_finalize<1><<<R, 64, 0, g->s_br>>>(FinalArgs{}, d_fin, 6);
-    NFSP_LAUNCHED("k_finalize");
+    if (snap_after) NFSP_HIP(hipEventRecord(g->snap_ev[par][1], g->s_br));
     // AR stream: the exchange when due (after this call's AR chains; AR nets only, so no other
     // stream touches what it writes), then the AR nets into snapshot `par`
     NFSP_HIP(hipStreamWaitEvent(g->s_ar, fork, 0));
     if (g->xchg_every > 0 && (++g->calls) % g->xchg_every == 0 && (rc = group_xchg_launch(g, g->s_ar)) != NFSP_OK)
       return rc;
     if (snap_after) {
-      if ((rc = nfsp::eng::group_snap_part_launch(g->eng.data(), R, g->d_roll, par, 1, g->s_br)) != NFSP_OK) return rc;
-      NFSP_HIP(hipEventRecord(g->snap_ev[par][1], g->s_br));
       if ((rc = nfsp::eng::group_snap_part_launch(g->eng.data(), R, g->d_roll, par, 0, g->s_ar)) != NFSP_OK) return rc;
       NFSP_HIP(hipEventRecord(g->snap_ev[par][0], g->s_ar));
     }
