@@ -191,3 +191,24 @@ def test_group_trace_records_every_slice_plan(pkg):
             assert t[:, r, a, 1].sum() == after[r]["br_updates"][a] - before[r]["br_updates"][a]
             assert t[:, r, a, 0].sum() >= after[r]["ar_updates"][a] - before[r]["ar_updates"][a]
     g.close()
+
+
+def test_pipelined_group_with_br_partitions_is_deterministic(pkg):
+    """A sliced, pipelined group (slice_lag 2) runs its BR jobs in 2 partitions on their own
+    streams, each partition going on into the next slice while the other finishes; every
+    partition takes its replicas' BR results and snapshot itself before its next chains.  Two
+    runs from the same seeds give the same nets bit for bit (a snapshot taken after the join,
+    while a partition already ran the next slice's chains, moved C4's learning curve)."""
+    kw = dict(n_lanes=65_536, slices=16, slice_lag=2, rl_capacity=200_000, sl_capacity=400_000)
+    runs = []
+    for _ in range(2):
+        g = pkg.engine.EngineGroup(4, seed=4242, init_seed=3, **kw)
+        g.set_exchange(pkg.native.XCHG_AR, every=1, scale=2.0 / 4)
+        g.average_ar()
+        for _ in range(3):
+            g.step()
+        assert min(g.stats()["br_updates"]) > 500
+        runs.append([x.copy() for r in g.replicas for x in nets(r)])
+        g.close()
+    for x, y in zip(*runs):
+        assert np.array_equal(x, y)
