@@ -899,8 +899,9 @@ struct nfsp_group {
   unsigned flags = 0;
   std::vector<nfsp_engine*> eng;
   hipStream_t s_ar = nullptr, s_br = nullptr;
-  // further BR streams: a sliced group's BR jobs run in GROUP_BR_STREAMS partitions, each its
-  // own rounds on its own stream (partition 0 on s_br)
+  // further BR streams: a sliced group's BR jobs run in up to GROUP_BR_STREAMS partitions,
+  // each its own rounds on its own stream (partition 0 on s_br); created on first use, so a
+  // group with one partition holds no extra stream (and no extra hardware queue)
   hipStream_t s_brp[GROUP_BR_STREAMS - 1] = {};
   void* d_roll = nullptr;        // the replicas' rollout arguments (static device table)
   // per learner call: job / prep / final tables, host (pinned) staging -> device, one copy;
@@ -996,8 +997,7 @@ extern "C" int nfsp_group_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, int 
     }
     g->eng.push_back(e);
   }
-  static_assert(GROUP_BR_STREAMS == 4, "the streams created below");
-  for (hipStream_t* st : {&g->s_ar, &g->s_br, &g->s_brp[0], &g->s_brp[1], &g->s_brp[2]}) {
+  for (hipStream_t* st : {&g->s_ar, &g->s_br}) {
     const hipError_t sr = hipStreamCreateWithFlags(st, hipStreamNonBlocking);
     if (sr != hipSuccess) {
       nfsp_group_destroy(g);
@@ -1296,6 +1296,9 @@ static int group_update(nfsp_group* g, bool pipelined = false, int par = 0, bool
     if ((rc = launch_ar(nullptr)) != NFSP_OK) return rc;
     ar_launched = true;
   }
+  for (int p = 1; p < nbs; ++p)
+    if (!g->s_brp[p - 1]) NFSP_HIP(hipStreamCreateWithFlags(&g->s_brp[p - 1], hipStreamNonBlocking));
+  static_assert(GROUP_BR_STREAMS == 4, "sp below");
   hipStream_t sp[GROUP_BR_STREAMS] = {g->s_br, g->s_brp[0], g->s_brp[1], g->s_brp[2]};
   for (int p = 0; p < nbs; ++p) NFSP_HIP(hipStreamWaitEvent(sp[p], fork_br, 0));
   KTimer kspan(e0, KT_BR_STREAM0, g->s_br);     // the group's BR streams, end to end (joined on s_br)
