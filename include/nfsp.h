@@ -441,7 +441,10 @@ int nfsp_group_set_timing(nfsp_group* g, int on);
  * count once each. */
 int nfsp_group_get_timings(nfsp_group* g, double* ms /*[NFSP_TIMING_SLOTS]*/,
                            int64_t* launches /*[NFSP_TIMING_SLOTS]*/);
-int nfsp_group_rounds(nfsp_group* g, int64_t* out);   /* BR rounds of the last learner call */
+/* BR rounds of the last learner call: the most any BR partition ran.  Sliced groups split the
+ * replicas' BR jobs into 2 partitions (env NFSP_GROUP_BR_STREAMS, 1..4), each with its own
+ * rounds on its own stream; the SGD steps are the same as with one. */
+int nfsp_group_rounds(nfsp_group* g, int64_t* out);
 /* Diagnostic trace of the learner calls' plans (tools/c4_slice_spread.py: the lockstep cost of
  * a per-slice exchange across C4 ranks).  on = 1 clears and starts it; every learner call then
  * appends, per replica r and agent a, its AR and BR update counts: [call][r][a][AR, BR].
