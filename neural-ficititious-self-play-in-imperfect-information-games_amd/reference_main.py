@@ -24,7 +24,7 @@ Then the file runs as ``__main__`` (``runpy.run_path``) in its own directory, wi
 the file is edited.  The per-decision calls go through libnfsp (``leduc.Env``,
 ``agent.Agent``); the loop itself is main.py's Python, ~1.3k hands/s.
 
-    python tools/run_reference_main.py /path/to/reference/main.py --episodes 2000
+    python tools/run_reference_main.py /path/to/reference/main.py --episodes 2000 [-- main.py's args]
 
 ``modules`` (tests only) replaces what ``install_dropin`` registers, e.g. by the CPU
 oracle's classes where there is no GPU.
@@ -172,14 +172,15 @@ def run(main_py: str, episodes: int | None = None, argv=(), overrides: dict | No
 
 
 def main(argv=None):
+    """CLI: ``<main.py> [--episodes N] [--sleep] [--plot-to PATH] [-- <main.py's own args>]``."""
+    argv = list(sys.argv[1:] if argv is None else argv)
+    own, rest = (argv[:argv.index("--")], argv[argv.index("--") + 1:]) if "--" in argv else (argv, [])
     ap = argparse.ArgumentParser(description="Run the reference's unchanged main.py on the MI355X drop-in.")
     ap.add_argument("main_py", help="path to the reference's main.py")
     ap.add_argument("--episodes", type=int, default=None, help="override [Common] Episodes")
     ap.add_argument("--sleep", action="store_true", help="keep main.py's time.sleep(60) at the end")
     ap.add_argument("--plot-to", default=None, help="plt.show() writes the curve to PATH.csv / PATH.png")
-    ap.add_argument("rest", nargs=argparse.REMAINDER, help="arguments passed to main.py")
-    a = ap.parse_args(argv)
-    rest = a.rest[1:] if a.rest[:1] == ["--"] else a.rest
+    a = ap.parse_args(own)
     out = run(a.main_py, episodes=a.episodes, argv=rest, skip_sleep=not a.sleep, plot_to=a.plot_to)
     if out["curves"]:
         print(f"exploitability-proxy curve: {len(out['curves'][-1])} points", flush=True)

@@ -80,3 +80,17 @@ def test_reference_main_py_runs_unchanged(pkg, capsys, tmp_path):
     p2 = orc.Agent(None, env.observation_space, env.action_space, "Player1", env)
     ref = orc.train(env, p1, p2, episodes)
     assert curve == ref
+
+
+def test_cli_splits_its_own_options_from_main_py_args(pkg, monkeypatch):
+    seen = {}
+
+    def fake_run(main_py, episodes=None, argv=(), skip_sleep=True, plot_to=None, **kw):
+        seen.update(main_py=main_py, episodes=episodes, argv=list(argv), skip_sleep=skip_sleep, plot_to=plot_to)
+        return {"curves": [], "tf_seeds": [], "globals": {}}
+
+    monkeypatch.setattr(pkg.reference_main, "run", fake_run)
+    assert pkg.reference_main.main(["m.py", "--episodes", "10", "--plot-to", "c", "--", "--human"]) == 0
+    assert seen == dict(main_py="m.py", episodes=10, argv=["--human"], skip_sleep=True, plot_to="c")
+    pkg.reference_main.main(["m.py", "--sleep"])
+    assert seen["argv"] == [] and seen["episodes"] is None and not seen["skip_sleep"]
