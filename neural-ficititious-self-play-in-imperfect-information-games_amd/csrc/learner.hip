@@ -1146,6 +1146,7 @@ static int group_update(nfsp_group* g, bool pipelined = false, int par = 0, bool
   // resume from the weights in memory: the same SGD steps, bit for bit.
   static const int cap_env = getenv("NFSP_GROUP_BR_CAP") ? atoi(getenv("NFSP_GROUP_BR_CAP")) : -1;
   const int64_t cap = cap_env >= 0 ? cap_env : (e0->slices > 1 ? 40 : 0);
+  static const bool pace_br = !(getenv("NFSP_GROUP_BR_PACE") && atoi(getenv("NFSP_GROUP_BR_PACE")) == 0);
   // Partitions: replicas [pr0[p], pr0[p + 1]) are partition p, whose BR jobs run their own
   // rounds on their own stream, followed (pipelined) by the partition's BR results and BR
   // snapshot on that stream.  A round then waits only for the longest piece among its
@@ -1181,10 +1182,31 @@ static int group_update(nfsp_group* g, bool pipelined = false, int par = 0, bool
     for (int r = pr0[p]; r < pr0[p + 1]; ++r)
       for (int a = 0; a < 2; ++a)
         if (!L[r].seg[a].empty()) bc.push_back({r, a, 0, L[r].seg[a][0].u});
+    // Paced pieces (capped groups): the partition's busiest job (most BR updates in this call)
+    // splits each of its segments into equal pieces of at most `cap`, and in every round the
+    // other jobs take at most the busiest job's piece of that round, so no round outlasts the
+    // busiest job's own piece and its last piece of a segment is not a short one.  (Plain caps:
+    // a 150-update segment ran as 40 + 40 + 40 + 30, and every job's round took 40.)
+    std::vector<int64_t> pace;                 // the busiest job's piece per round
+    if (cap > 0 && pace_br) {
+      int64_t most = -1;
+      const std::vector<Segment>* bs = nullptr;
+      for (const BrCursor& c : bc) {
+        int64_t n = 0;
+        for (const Segment& sg : L[c.r].seg[c.a]) n += sg.v - sg.u;
+        if (n > most) most = n, bs = &L[c.r].seg[c.a];
+      }
+      if (bs)
+        for (const Segment& sg : *bs) {
+          const int64_t len = sg.v - sg.u, np = (len + cap - 1) / cap;
+          for (int64_t k = 0; k < np; ++k) pace.push_back(len / np + (k < len % np ? 1 : 0));
+        }
+    }
     int64_t nr = 0;
     for (;;) {
       const size_t b0 = br_jobs.size(), t0 = tg_jobs.size();
       int64_t rn = 0;
+      const int64_t pk = (size_t)nr < pace.size() ? pace[(size_t)nr] : cap;
       for (BrCursor& c : bc) {
         const std::vector<Segment>& segs = L[c.r].seg[c.a];
         if (c.s >= segs.size()) continue;
@@ -1193,7 +1215,7 @@ static int group_update(nfsp_group* g, bool pipelined = false, int par = 0, bool
           tg_jobs.push_back(br_target_job(g->eng[c.r], L[c.r], c.a, sg));
           rn = sg.v - sg.u > rn ? sg.v - sg.u : rn;
         }
-        const int64_t end = cap > 0 && c.pos + cap < sg.v ? c.pos + cap : sg.v;
+        const int64_t end = pk > 0 && c.pos + pk < sg.v ? c.pos + pk : sg.v;
         br_jobs.push_back(br_chain_job(g->eng[c.r], c.a, Segment{c.pos, end, sg.sync && end == sg.v}));
         c.pos = end;
         if (end == sg.v && ++c.s < segs.size()) c.pos = segs[c.s].u;
