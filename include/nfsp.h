@@ -406,9 +406,14 @@ int nfsp_engine_set_update_limit(nfsp_engine* e, int64_t max_updates);
  * its own nets.  Replica r uses cfg.seed + r, and is bit-identical to a standalone engine
  * created with that seed and stepped as often.  nfsp_group_step does rollout + update for
  * every replica.  The SGD chains of all replicas run in shared launches: one AR launch of 2R
- * workgroups; the BR chains in rounds, where round k holds every (replica, agent)'s k-th
- * target-sync segment.  A chain workgroup occupies one CU, so one learner pair's 4 CUs
- * become 4R.  This is BASELINE C4's shard model inside one GPU.
+ * workgroups; the BR chains in rounds of one targets launch and one chain launch.  Unsliced,
+ * round k holds every (replica, agent)'s k-th target-sync segment; sliced (cfg.slices > 1),
+ * the replicas are split into 2 halves with their own rounds on their own streams, and a
+ * round's pieces are at most 40 updates, paced by the half's busiest job (env
+ * NFSP_GROUP_BR_CAP / NFSP_GROUP_BR_PACE / NFSP_GROUP_BR_STREAMS).  A piece
+ * resumes from the weights in memory, so the SGD steps are a standalone engine's.  A chain
+ * workgroup occupies one CU, so one learner pair's 4 CUs become 4R.  This is BASELINE C4's
+ * shard model inside one GPU.
  * With NFSP_GROUP_AVG_AR, replica 0's AR nets are first copied to every replica.  After every
  * step, each AR net becomes W0 + sum_r (W_r - W0) / R, with W0 = the nets after the
  * previous exchange.  This is shards.AvgPolicyAllReduce's per-step exchange, done on device.
