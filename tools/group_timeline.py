@@ -16,8 +16,8 @@ sys.path.insert(0, REPO)
 
 
 def main():
+    import bench          # first: it sets GPU_MAX_HW_QUEUES (8) before anything initialises HIP
     import torch
-    import bench
     pkg = __import__("__graft_entry__").load_package()
     name = sys.argv[1] if len(sys.argv) > 1 else "c4_emul_r8"
     warmup = int(sys.argv[2]) if len(sys.argv) > 2 else 1
