@@ -109,23 +109,32 @@ def configparser_stub(overrides: dict | None = None) -> types.ModuleType:
     return mod
 
 
+def time_stub() -> types.ModuleType:
+    """``time`` for the run: everything is the real module's except ``sleep``, which returns at
+    once (main.py:124 sleeps 60 s after plt.show()).  The real module is left alone, so other
+    threads' sleeps are untouched."""
+    mod = types.ModuleType("time")
+    mod.__dict__.update({k: v for k, v in vars(time).items() if not k.startswith("__")})
+    mod.sleep = lambda seconds: None
+    return mod
+
+
 @contextlib.contextmanager
 def _patched(modules: dict, argv: list, cwd: str, skip_sleep: bool):
+    if skip_sleep:
+        modules = dict(modules, time=time_stub())
     saved_mods = {k: sys.modules.get(k) for k in modules}
-    saved_argv, saved_cwd, saved_sleep = sys.argv, os.getcwd(), time.sleep
+    saved_argv, saved_cwd = sys.argv, os.getcwd()
     root = logging.getLogger()             # main.py:12 basicConfig(level=DEBUG) on the root logger
     saved_log = (root.level, list(root.handlers))
     try:
         sys.modules.update(modules)
         sys.argv = argv
         os.chdir(cwd)
-        if skip_sleep:
-            time.sleep = lambda s: None
         yield
     finally:
         root.setLevel(saved_log[0])
         root.handlers[:] = saved_log[1]
-        time.sleep = saved_sleep
         os.chdir(saved_cwd)
         sys.argv = saved_argv
         for k, v in saved_mods.items():
@@ -141,7 +150,8 @@ def run(main_py: str, episodes: int | None = None, argv=(), overrides: dict | No
 
     episodes: overrides ``[Common] Episodes`` of its config.ini (main.py:27);
     overrides: further ``{(section, option): value}`` for its ConfigParser;
-    skip_sleep: the ``time.sleep(60)`` after ``plt.show()`` (main.py:124) returns at once;
+    skip_sleep: the ``time.sleep(60)`` after ``plt.show()`` (main.py:124) returns at once (the
+      file's ``import time`` gets ``time_stub()``);
     plot_to: the curve ``plt.show()`` was asked to show goes to <plot_to>.csv / .png;
     modules: replaces the drop-in's module registrations (tests: the CPU oracle's classes).
     Returns ``{"globals": the module's globals, "curves": what it passed to plt.plot,

@@ -46,6 +46,9 @@ def test_stubs_cover_what_main_py_uses(pkg):
     plt.plot([1.0, 2.0])
     plt.show()
     assert plt.curves == [[1.0, 2.0]] and plt.shown == 1 and mpl.pyplot is plt
+    import time
+    ts = rm.time_stub()
+    assert ts.sleep(60) is None and ts.time is time.time and time.sleep is not ts.sleep
     cp = rm.configparser_stub({("Common", "Episodes"): 7}).ConfigParser()
     cp.read_string("[Common]\nEpisodes: 400000\n[Agent]\nEta: 0.1\n")
     assert cp.get("Common", "Episodes") == "7" and cp.get("Agent", "Eta") == "0.1"
