@@ -564,6 +564,9 @@ def stub_main(args, world, rank, dist):
         xcheck["after_timed_pass"] = check_ar_nets(dist, digest(), "after the timed pass")
         out["ar_allreduce"] = dict(check_exchange_calls(c1 - c0, args.steps, slices, 1), calls=calls[0],
                                    transport="stub", fallback=fallback, ar_nets_check=xcheck)
+        # the stand-in net's "exploitability" is a placeholder; the hands are the protocol's
+        out["ar_allreduce"]["learning_at_total_hands"] = learning_check(
+            1.0, (args.warmup + args.steps) * lanes, world, True)
     if dist is not None:
         import socket
         out["ranks"] = rank_report(dist, "gloo", dict(
@@ -605,6 +608,16 @@ def band_check(x: float, hands: int) -> dict:
     if b is not None:
         out["sigmas_from_cpu_mean"] = (x - b["mean"]) / b["std"]
         out["inside_bar"] = abs(x - b["mean"]) <= 2 * b["std"] and x <= b["mean"] + b["std"]
+    return out
+
+
+def learning_check(x: float, hands_per_rank: int, world: int, exchanged: bool) -> dict:
+    """band_check at the hands the evaluated net has learned from: with the AR exchange on, the
+    ranks' AR nets are one net trained on every rank's hands, so the job's TOTAL hands (world x
+    per rank) -- the x-axis of the C4 gate (tests/test_gpu_slices.py) and of the CPU band; without
+    it, one shard's own hands."""
+    out = band_check(x, hands_per_rank * world if exchanged else hands_per_rank)
+    out["hands_are"] = "total over ranks (the exchanged AR net)" if exchanged else "this rank's"
     return out
 
 
@@ -672,11 +685,16 @@ def measure_group(pkg, name: str, steps: int, warmup: int) -> dict:
     return out
 
 
-def rooflines(config, cfg, k_ms, k_launches, k_step_ms, br_upd, ar_upd, ar_max, t_rl, t_sl, hands_per_s):
+def rooflines(config, cfg, k_ms, k_launches, k_step_ms, br_upd, ar_upd, ar_max, t_rl, t_sl, hands_per_s,
+              ms_per_step=None):
     """SURVEY 8(d)'s framings of the kernels, from one event-timed pass: k_ms = average ms per
     launch, k_launches = launches, k_step_ms = ms per engine step (per kernel / stream);
     br_upd / ar_upd = the pass's BR / AR updates (both agents), ar_max = the longest AR chain's
     updates; t_rl / t_sl = RL / SL inserts per hand; hands_per_s = the un-instrumented rate.
+    ms_per_step: the un-instrumented pass's step time.  The headline kernel's duration is then
+    capped by it: the critical stream runs its launches back to back, so one launch lasts at
+    most the un-instrumented step / launches per step; the events around every launch add
+    ~0.8 %, and the line's kernel time must not exceed its step time.
     Returns (roofline, roofline_other, whole_step_hbm_per_gpu, stream_ms_per_step).
     tests/test_bench_roofline.py feeds it the committed profiles' timings."""
     R = cfg.get("replicas", 1)
@@ -779,6 +797,16 @@ def rooflines(config, cfg, k_ms, k_launches, k_step_ms, br_upd, ar_upd, ar_max, 
     roof_key = f"{dom}_hbm"
     roofline = dict(roofs[roof_key])
     roofline["critical_stream"] = crit
+    per_step = k_step_ms[dom] / k_ms[dom] if k_ms[dom] > 0 else 0.0      # launches per step
+    roofline["launches_per_step"] = per_step
+    roofline["avg_ms_event_timed"] = k_ms[dom]
+    roofline["avg_ms_source"] = "HIP events around every launch (second pass)"
+    if ms_per_step and per_step > 0 and ms_per_step / per_step < k_ms[dom]:
+        roofline["avg_ms"] = ms_per_step / per_step
+        roofline["avg_ms_source"] = ("un-instrumented step / launches per step on the critical stream "
+                                     "(the event-timed average is longer: events around every launch)")
+        roofline["achieved"] = roofline["bytes_per_launch"] / (roofline["avg_ms"] * 1e-3) / 1e9
+        roofline["frac"] = roofline["achieved"] / PEAK_HBM_GBS
     pmc = load_pmc(config, roofline["kernel"])
     if pmc is not None:
         roofline["traffic"] = pmc
@@ -836,6 +864,11 @@ def main():
         ap.error(f"{args.config} is a one-GPU group line: bench.py --groups {args.config}")
     args.xchg_every = args.xchg_every if args.xchg_every is not None else c.get("xchg_every", 1)
     args.xchg_gain = args.xchg_gain if args.xchg_gain is not None else c.get("xchg_gain", 2.0)
+    slices = args.slices if args.slices is not None else c.get("slices", 1)
+    if args.xchg_every < 1 or slices % args.xchg_every:
+        # every step must end on an exchange: the AR-net digest check after the warmup and after
+        # the timed pass compares the ranks' nets, which agree only right after an exchange
+        ap.error(f"--xchg-every {args.xchg_every} must divide the config's {slices} slices")
 
     if args.cpu_worker:                # a CPU-baseline child process: no GPU, one JSON line
         print(json.dumps(cpu_worker(args.cpu_worker, args.cpu_seconds, args.config, args.cpu_seed,
@@ -926,7 +959,7 @@ def main():
     ar_max = max(b["ar_updates"][a] - x["ar_updates"][a] for x, b in zip(reps1, reps2) for a in (0, 1))
     roofline, roofs_other, whole_step, streams = rooflines(
         args.config, cfg, k_ms, k_launches, k_step_ms, br_upd, ar_upd, ar_max, t_rl, t_sl,
-        hands_rank / elapsed)
+        hands_rank / elapsed, ms_per_step=elapsed / args.steps * 1e3)
     rollout_path_ms = k_step_ms["k_rollout"] + k_step_ms["k_scan"] + k_step_ms["k_commit"]
     out = {
         "metric": "Kuhn self-play hands/sec" if cfg.get("game") == "kuhn" else "Leduc self-play hands/sec",
@@ -987,8 +1020,13 @@ def main():
         "softmax_mixed": ex[0]["exploitability"], "argmax_as_executed": ex[1]["exploitability"],
         "hands_trained_per_gpu": int(s2["hands"]), "unit": "chips (BR_0 + BR_1)"}
     if cfg.get("game", "leduc") == "leduc" and cfg["rl_capacity"] == 200_000:
-        # the CPU reference's seed band at the same hands (one seed of the engine here)
-        out["exploitability_exact"]["vs_cpu_band"] = band_check(ex[0]["exploitability"], int(s2["hands"]))
+        # the CPU reference's seed band at the same hands (one seed of the engine here): at N > 1
+        # with the exchange on, the total hands of the job (the AR net learned from all of them)
+        exchanged = avg is not None and world > 1
+        chk = learning_check(ex[0]["exploitability"], int(s2["hands"]), world, exchanged)
+        out["exploitability_exact"]["vs_cpu_band"] = chk
+        if exchanged:
+            out["ar_allreduce"]["learning_at_total_hands"] = chk
     if world == 1 and args.config == "c3" and args.groups:
         # several learners on the one GPU (engine groups): new measured configs, not the headline
         eng.close()

@@ -267,7 +267,13 @@ typedef struct nfsp_engine_cfg {
    * and epsilon its learner left after slice j - 2 (snapshots on device): the same arithmetic
    * as a pipelined engine, not its overlap. */
   int32_t slice_lag;
+  /* Scheduling flags (NFSP_SCHED_*; they change only the order of launches, never a result).
+   * nfsp_engine_default_cfg takes them from the environment (NFSP_LEARNER_SERIAL=1), read at
+   * that call; 0 = the production schedule. */
+  uint32_t sched;
 } nfsp_engine_cfg;
+/* diagnostic: an engine's BR work waits for its AR chains, to time each alone */
+#define NFSP_SCHED_LEARNER_SERIAL 1u
 
 typedef struct nfsp_engine_stats {
   int64_t hands, rollouts;
@@ -409,8 +415,8 @@ int nfsp_engine_set_update_limit(nfsp_engine* e, int64_t max_updates);
  * workgroups; the BR chains in rounds of one targets launch and one chain launch.  Unsliced,
  * round k holds every (replica, agent)'s k-th target-sync segment; sliced (cfg.slices > 1),
  * the replicas are split into 2 halves with their own rounds on their own streams, and a
- * round's pieces are at most 40 updates, paced by the half's busiest job (env
- * NFSP_GROUP_BR_CAP / NFSP_GROUP_BR_PACE / NFSP_GROUP_BR_STREAMS).  A piece
+ * round's pieces are at most 40 updates, paced by the half's busiest job (nfsp_group_sched;
+ * DESIGN.md 4.5).  A piece
  * resumes from the weights in memory, so the SGD steps are a standalone engine's.  A chain
  * workgroup occupies one CU, so one learner pair's 4 CUs become 4R.  This is BASELINE C4's
  * shard model inside one GPU.
@@ -441,13 +447,31 @@ int nfsp_group_average_ar(nfsp_group* g);
 #define NFSP_XCHG_AR 1u
 #define NFSP_XCHG_BR 2u
 int nfsp_group_set_exchange(nfsp_group* g, unsigned nets, int every, float scale);
+/* How a group schedules its BR rounds and slices.  None of these changes an SGD
+ * step: a BR piece resumes from the weights in memory, and every partition's jobs run the same
+ * pieces and targets (tests/test_gpu_group.py varies them within one process).
+ *   br_cap      most updates per BR piece; -1: 40 for sliced groups, whole segments (0) else
+ *   br_pace     1: a partition's busiest job splits each segment into equal pieces and the
+ *               others follow its piece per round; 0: plain caps
+ *   br_streams  BR partitions, each its own rounds on its own stream (1..4); -1: 2 for sliced
+ *               groups, else 1 (always 1 when chains share CUs)
+ *   serial      1: the slices of a pipelined group run one after another (no overlap)
+ * nfsp_group_default_sched reads the environment's NFSP_GROUP_BR_CAP / _BR_PACE / _BR_STREAMS /
+ * NFSP_GROUP_SERIAL at that call (nfsp_group_create starts from it); nfsp_group_set_sched
+ * applies from the next learner call. */
+typedef struct nfsp_group_sched {
+  int32_t br_cap, br_pace, br_streams, serial;
+} nfsp_group_sched;
+int nfsp_group_default_sched(nfsp_group_sched* out);
+int nfsp_group_set_sched(nfsp_group* g, const nfsp_group_sched* sched);
+int nfsp_group_get_sched(nfsp_group* g, nfsp_group_sched* out);
 int nfsp_group_set_timing(nfsp_group* g, int on);
 /* nfsp_engine_get_timings summed over the replicas.  The shared chain and target launches
  * count once each. */
 int nfsp_group_get_timings(nfsp_group* g, double* ms /*[NFSP_TIMING_SLOTS]*/,
                            int64_t* launches /*[NFSP_TIMING_SLOTS]*/);
 /* BR rounds of the last learner call: the most any BR partition ran.  Sliced groups split the
- * replicas' BR jobs into 2 partitions (env NFSP_GROUP_BR_STREAMS, 1..4), each with its own
+ * replicas' BR jobs into 2 partitions (nfsp_group_sched.br_streams, 1..4), each with its own
  * rounds on its own stream; the SGD steps are the same as with one. */
 int nfsp_group_rounds(nfsp_group* g, int64_t* out);
 /* Diagnostic trace of the learner calls' plans (tools/c4_slice_spread.py: the lockstep cost of

@@ -521,6 +521,8 @@ extern "C" int nfsp_engine_default_cfg(nfsp_engine_cfg* c) {
   c->seed = 1234;
   c->slices = 1;
   c->slice_lag = 1;
+  const char* ls = getenv("NFSP_LEARNER_SERIAL");
+  c->sched = ls && atoi(ls) ? NFSP_SCHED_LEARNER_SERIAL : 0u;
   return NFSP_OK;
 }
 

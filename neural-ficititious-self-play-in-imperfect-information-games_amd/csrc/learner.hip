@@ -731,8 +731,9 @@ static int update_impl(nfsp_engine* e, bool pipelined, int par, bool snap_after)
     NFSP_LAUNCHED("k_finalize");
   }
   float* snap = e->snap + (size_t)par * 6 * nn::NP;
-  // diagnostic (NFSP_LEARNER_SERIAL=1): BR work waits for the AR chains, to time them alone
-  static const bool serial_ar = getenv("NFSP_LEARNER_SERIAL") && atoi(getenv("NFSP_LEARNER_SERIAL"));
+  // diagnostic (cfg.sched NFSP_SCHED_LEARNER_SERIAL): BR work waits for the AR chains, to time
+  // them alone
+  const bool serial_ar = (e->cfg.sched & NFSP_SCHED_LEARNER_SERIAL) != 0;
   hipEvent_t ar_done = fork;
   // ---- AR chains (both agents, one launch) on their own stream.  With the exchange on and
   // the slices pipelined, this call's exchange (and the AR snapshot it feeds) is enqueued by
@@ -891,7 +892,7 @@ int step_pipelined(nfsp_engine* e) {
 // ---------------------------------------------------------------------------
 // Engine groups (nfsp_group_*): R replicas stepped together, their chains in shared launches
 // ---------------------------------------------------------------------------
-constexpr int GROUP_BR_STREAMS = 4;   // at most; NFSP_GROUP_BR_STREAMS (group_update)
+constexpr int GROUP_BR_STREAMS = 4;   // at most; nfsp_group_sched.br_streams (group_update)
 
 struct nfsp_group {
   nfsp_ctx* ctx = nullptr;
@@ -923,6 +924,7 @@ struct nfsp_group {
   float xchg_scale = 1.f;
   int64_t calls = 0;             // learner calls (slices) so far
   int64_t rounds = 0;            // BR rounds of the last learner call (stats)
+  nfsp_group_sched sched{};      // nfsp_group_set_sched (from nfsp_group_default_sched)
   int chain_lds = 0;             // LDS per chain workgroup: 4R chains on the device's CUs
   bool trace_on = false;         // nfsp_group_set_trace: per call [R][2][AR, BR] update counts
   std::vector<int32_t> trace;
@@ -986,6 +988,7 @@ extern "C" int nfsp_group_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, int 
     g->xchg_scale = 1.0f / (float)replicas;
   }
   g->chain_lds = chain_lds_shared((4 * replicas + cus - 1) / (cus > 0 ? cus : 1));
+  nfsp_group_default_sched(&g->sched);
   for (int r = 0; r < replicas; ++r) {
     nfsp_engine_cfg c = *cfg;
     c.seed = cfg->seed + (uint64_t)r;
@@ -1144,20 +1147,20 @@ static int group_update(nfsp_group* g, bool pipelined = false, int par = 0, bool
   // waits for the longest segment of every round: a sliced group's BR stream ran 1.9 ms per
   // slice against 1.2 ms for its busiest job (tools/group_timeline.py).  Pieces of a segment
   // resume from the weights in memory: the same SGD steps, bit for bit.
-  static const int cap_env = getenv("NFSP_GROUP_BR_CAP") ? atoi(getenv("NFSP_GROUP_BR_CAP")) : -1;
-  const int64_t cap = cap_env >= 0 ? cap_env : (e0->slices > 1 ? 40 : 0);
-  static const bool pace_br = !(getenv("NFSP_GROUP_BR_PACE") && atoi(getenv("NFSP_GROUP_BR_PACE")) == 0);
+  const int64_t cap = g->sched.br_cap >= 0 ? g->sched.br_cap : (e0->slices > 1 ? 40 : 0);
+  const bool pace_br = g->sched.br_pace != 0;
   // Partitions: replicas [pr0[p], pr0[p + 1]) are partition p, whose BR jobs run their own
   // rounds on their own stream, followed (pipelined) by the partition's BR results and BR
   // snapshot on that stream.  A round then waits only for the longest piece among its
-  // partition's jobs, one partition's targets overlap the others' chains, and a partition goes
-  // on into the next slice without waiting for the others.  Each job's pieces and targets are
+  // partition's jobs, and one partition's targets overlap the others' chains.  Partitions
+  // 1.. go on into the next slice without waiting for the others; partition 0 runs on s_br,
+  // which joins every partition at the end of the call (below), so its next-slice rounds wait
+  // for the slowest partition: the overlap is asymmetric.  Each job's pieces and targets are
   // the same as with one partition, so are its SGD steps.  Sliced groups only (their rounds
   // are short: the targets between them were ~10% of c4_emul_r8's BR stream); groups whose
   // chains share CUs keep one stream.
   const bool shared_cus = g->chain_lds < CHAIN_LDS;
-  static const int nbs_env = getenv("NFSP_GROUP_BR_STREAMS") ? atoi(getenv("NFSP_GROUP_BR_STREAMS")) : -1;
-  int nbs = nbs_env > 0 ? nbs_env : (e0->slices > 1 ? 2 : 1);
+  int nbs = g->sched.br_streams > 0 ? g->sched.br_streams : (e0->slices > 1 ? 2 : 1);
   nbs = nbs > GROUP_BR_STREAMS ? GROUP_BR_STREAMS : nbs;
   nbs = nbs > R ? R : nbs;
   if (shared_cus) nbs = 1;
@@ -1453,9 +1456,8 @@ extern "C" int nfsp_group_step(nfsp_group* g) {
   // Pipelined (as step_pipelined): slice j's rollout waits only for the snapshot copies of
   // slice j - 2, so the rollout, readback, plan and prep of slice j + 1 overlap slice j's
   // chains.  The same arithmetic as the serial loop below.  Not with a BR exchange (it would
-  // need both learner streams joined after every exchange) or NFSP_GROUP_SERIAL=1.
-  static const bool serial_env = getenv("NFSP_GROUP_SERIAL") && atoi(getenv("NFSP_GROUP_SERIAL"));
-  if (lag2 && !(g->xchg_nets & NFSP_XCHG_BR) && !serial_env) {
+  // need both learner streams joined after every exchange) or sched.serial.
+  if (lag2 && !(g->xchg_nets & NFSP_XCHG_BR) && !g->sched.serial) {
     hipStream_t s = g->ctx->stream;
     if ((rc = nfsp::eng::group_snap_launch(g->eng.data(), g->R, g->d_roll, -1)) != NFSP_OK) return rc;
     for (int j = 0; j < K; ++j) {
@@ -1483,6 +1485,39 @@ extern "C" int nfsp_group_step(nfsp_group* g) {
     if (lag2 && j + 2 < K && (rc = nfsp::eng::group_snap_launch(g->eng.data(), g->R, g->d_roll, j & 1)) != NFSP_OK)
       return rc;
   }
+  return NFSP_OK;
+}
+
+namespace {
+int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : dflt;
+}
+}  // namespace
+
+extern "C" int nfsp_group_default_sched(nfsp_group_sched* out) {
+  NFSP_REQUIRE(out, "null argument");
+  out->br_cap = env_int("NFSP_GROUP_BR_CAP", -1);
+  out->br_pace = env_int("NFSP_GROUP_BR_PACE", 1) != 0;
+  out->br_streams = env_int("NFSP_GROUP_BR_STREAMS", -1);
+  out->serial = env_int("NFSP_GROUP_SERIAL", 0) != 0;
+  return NFSP_OK;
+}
+
+extern "C" int nfsp_group_set_sched(nfsp_group* g, const nfsp_group_sched* sc) {
+  NFSP_REQUIRE(g && sc, "null argument");
+  NFSP_REQUIRE(sc->br_cap >= -1, "br_cap must be >= -1");
+  NFSP_REQUIRE(sc->br_streams == -1 || (sc->br_streams >= 1 && sc->br_streams <= GROUP_BR_STREAMS),
+               "br_streams must be -1 or in [1, 4]");
+  g->sched = *sc;
+  g->sched.br_pace = sc->br_pace != 0;
+  g->sched.serial = sc->serial != 0;
+  return NFSP_OK;
+}
+
+extern "C" int nfsp_group_get_sched(nfsp_group* g, nfsp_group_sched* out) {
+  NFSP_REQUIRE(g && out, "null argument");
+  *out = g->sched;
   return NFSP_OK;
 }
 

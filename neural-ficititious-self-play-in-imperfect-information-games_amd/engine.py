@@ -266,7 +266,7 @@ class EngineGroup:
     after every slice, shards.AvgPolicyExchange's).  ``slice_lag=2``: every replica's slice j
     acts with the nets slice j - 2 left (a pipelined engine's arithmetic; executed pipelined --
     slice j + 1's rollout, plan and prep overlap slice j's chains -- unless the BR nets are
-    exchanged or NFSP_GROUP_SERIAL=1)."""
+    exchanged or ``set_sched(serial=1)``)."""
 
     def __init__(self, replicas: int, ctx: native.Context | None = None, init_seed: int = 0,
                  game: int = native.GAME_LEDUC, avg_ar: bool = False, **cfg):
@@ -301,6 +301,23 @@ class EngineGroup:
         scale = 1.0 / self.R if scale is None else float(scale)
         native.check(self.L.nfsp_group_set_exchange(self.h, int(nets), int(every), scale),
                      "nfsp_group_set_exchange")
+
+    def sched(self) -> dict:
+        """The group's BR-round / slice schedule (nfsp_group_get_sched)."""
+        sc = native.GroupSched()
+        native.check(self.L.nfsp_group_get_sched(self.h, C.byref(sc)), "nfsp_group_get_sched")
+        return {k: int(getattr(sc, k)) for k, _ in sc._fields_}
+
+    def set_sched(self, **kw):
+        """nfsp_group_set_sched: change br_cap / br_pace / br_streams / serial from the next
+        learner call (the rest stay as they are).  No SGD step changes."""
+        cur = self.sched()
+        for k in kw:
+            if k not in cur:
+                raise KeyError(k)
+        cur.update(kw)
+        native.check(self.L.nfsp_group_set_sched(self.h, C.byref(native.GroupSched(**cur))),
+                     "nfsp_group_set_sched")
 
     def rounds(self) -> int:
         n = native.I64()

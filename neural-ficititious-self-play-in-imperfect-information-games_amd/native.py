@@ -40,7 +40,13 @@ class EngineCfg(C.Structure):
                 ("target_every", C.c_int32), ("epochs", C.c_int32), ("fit_batch", C.c_int32),
                 ("quirks", C.c_uint32), ("eta", F32), ("lr_br", F32), ("lr_ar", F32),
                 ("gamma", F64), ("epsilon", F64), ("seed", U64), ("slices", C.c_int32),
-                ("slice_lag", C.c_int32)]
+                ("slice_lag", C.c_int32), ("sched", C.c_uint32)]
+
+
+class GroupSched(C.Structure):
+    """``nfsp_group_sched``: how a group schedules its BR rounds and slices (no result changes)"""
+    _fields_ = [("br_cap", C.c_int32), ("br_pace", C.c_int32), ("br_streams", C.c_int32),
+                ("serial", C.c_int32)]
 
 
 class EngineStats(C.Structure):
@@ -123,6 +129,9 @@ SIGNATURES = {
     "nfsp_group_set_trace": (I32, [P, I32]),
     "nfsp_group_trace": (I32, [P, C.POINTER(I32), I64, C.POINTER(I64)]),
     "nfsp_group_set_exchange": (I32, [P, U32, I32, F32]),
+    "nfsp_group_default_sched": (I32, [C.POINTER(GroupSched)]),
+    "nfsp_group_set_sched": (I32, [P, C.POINTER(GroupSched)]),
+    "nfsp_group_get_sched": (I32, [P, C.POINTER(GroupSched)]),
     "nfsp_engine_set_exchange": (I32, [P, I32, F32, P, P, P]),
     "nfsp_engine_exchanges": (I32, [P, C.POINTER(I64)]),
     "nfsp_rccl_ready": (I32, [I32]),

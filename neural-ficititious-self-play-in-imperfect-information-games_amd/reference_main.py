@@ -110,19 +110,35 @@ def configparser_stub(overrides: dict | None = None) -> types.ModuleType:
 
 
 def time_stub() -> types.ModuleType:
-    """``time`` for the run: everything is the real module's except ``sleep``, which returns at
-    once (main.py:124 sleeps 60 s after plt.show()).  The real module is left alone, so other
-    threads' sleeps are untouched."""
+    """``time`` for main.py's own code: everything is the real module's except ``sleep``, which
+    returns at once (main.py:124 sleeps 60 s after plt.show()).  It is never put in sys.modules:
+    only main.py's ``import time`` gets it (``main_builtins``), so a module imported for the first
+    time during the run (the drop-in's, torch's) binds the real ``time``."""
     mod = types.ModuleType("time")
     mod.__dict__.update({k: v for k, v in vars(time).items() if not k.startswith("__")})
     mod.sleep = lambda seconds: None
     return mod
 
 
+def main_builtins(time_mod: types.ModuleType) -> dict:
+    """The builtins main.py's code runs with (its globals' ``__builtins__``): the real ones, but
+    ``import time`` returns ``time_mod``.  Every other module keeps the real builtins and the
+    real ``time`` (a stub in sys.modules would stick to whatever module was first
+    imported during the run)."""
+    import builtins
+    real_import = builtins.__import__
+
+    def _import(name, globals=None, locals=None, fromlist=(), level=0):
+        if name == "time" and level == 0:
+            return time_mod
+        return real_import(name, globals, locals, fromlist, level)
+    b = dict(vars(builtins))
+    b["__import__"] = _import
+    return b
+
+
 @contextlib.contextmanager
-def _patched(modules: dict, argv: list, cwd: str, skip_sleep: bool):
-    if skip_sleep:
-        modules = dict(modules, time=time_stub())
+def _patched(modules: dict, argv: list, cwd: str):
     saved_mods = {k: sys.modules.get(k) for k in modules}
     saved_argv, saved_cwd = sys.argv, os.getcwd()
     root = logging.getLogger()             # main.py:12 basicConfig(level=DEBUG) on the root logger
@@ -173,8 +189,9 @@ def run(main_py: str, episodes: int | None = None, argv=(), overrides: dict | No
     mpl, plt = matplotlib_stub()
     mods["matplotlib"], mods["matplotlib.pyplot"] = mpl, plt
     mods["ConfigParser"] = configparser_stub(ov)
-    with _patched(mods, [main_py, *argv], os.path.dirname(main_py), skip_sleep):
-        g = runpy.run_path(main_py, run_name="__main__")
+    init = {"__builtins__": main_builtins(time_stub())} if skip_sleep else None
+    with _patched(mods, [main_py, *argv], os.path.dirname(main_py)):
+        g = runpy.run_path(main_py, init_globals=init, run_name="__main__")
     if plot_to and plt.shown and plt.curves:       # after the stand-ins are gone (real pyplot)
         from .observability import save_curve
         save_curve(plt.curves[-1], plot_to + ".csv", plot_to + ".png", xlabel="report")

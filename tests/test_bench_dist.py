@@ -138,6 +138,37 @@ def test_n2_line_proves_its_exchange():
     chk = x["ar_nets_check"]
     assert chk["after_warmup"]["ar_nets_identical"] and chk["after_timed_pass"]["ar_nets_identical"]
     assert lines[0]["ranks"]["ar_nets_identical"] is True
+    # the exchanged AR net is scored at the job's TOTAL hands: 2 ranks x (1 + 3) steps x 65,536
+    lt = x["learning_at_total_hands"]
+    assert lt["hands"] == 2 * 4 * 65_536 and lt["hands_are"].startswith("total")
+    assert lt["cpu_band"]["hands"] == 0 or lt["cpu_band"]["hands"] % 2_000_000 == 0
+
+
+def test_n1_line_has_no_exchange_fields():
+    rc, lines, err = _bench(["--steps", "2", "--warmup", "1", "--stub-step-ms", "2", "--config", "c2"])
+    assert rc == 0, err
+    assert "ar_allreduce" not in lines[0]
+
+
+def test_learning_check_x_axis():
+    """bench.learning_check: per-rank hands without the exchange, world x hands with it."""
+    import bench
+    a = bench.learning_check(1.3, 8_388_608, 8, False)
+    b = bench.learning_check(1.3, 8_388_608, 8, True)
+    assert a["hands"] == 8_388_608 and a["cpu_band"]["hands"] == 8_000_000
+    assert b["hands"] == 67_108_864 and b["cpu_band"]["beyond_band"] is True
+
+
+def test_xchg_every_must_divide_the_slices():
+    """an --xchg-every that does not divide the slices would leave a step's last
+    slices unexchanged, and the AR-net digest check would end the job; it is refused up front."""
+    rc, lines, err = _bench(["--gpus", "2", "--steps", "2", "--warmup", "1", "--stub-step-ms", "2",
+                             "--config", "c2", "--xchg-every", "3"])
+    assert rc == 2 and not lines
+    assert "must divide" in err
+    rc, lines, err = _bench(["--steps", "1", "--warmup", "0", "--stub-step-ms", "2", "--config", "c2",
+                             "--xchg-every", "4"])
+    assert rc == 0, err
 
 
 def test_host_fallback_refused_under_rccl():

@@ -61,6 +61,21 @@ def test_every_frac_at_most_one(name, config):
     assert other["k_chain3_ar_mfma"]["peak"] == bench.PEAK_BF16_TFLOPS
 
 
+@pytest.mark.parametrize("name,config", PROFILES)
+def test_roofline_kernel_time_within_the_step(name, config):
+    """with the un-instrumented step time given, the headline kernel's
+    launches per step x avg_ms never exceed the step (within 0.5 %), and frac follows avg_ms."""
+    import bench
+    with open(os.path.join(REPO, "profiles", name)) as f:
+        d = json.load(f)
+    cfg = dict(bench.CONFIGS[config], slices=d.get("slices", 1), slice_lag=d.get("slice_lag", 1))
+    roof, _, _, _ = bench.rooflines(config, cfg, *_inputs(d), ms_per_step=d["ms_per_step"])
+    assert roof["launches_per_step"] * roof["avg_ms"] <= d["ms_per_step"] * 1.005, roof
+    assert roof["avg_ms"] <= roof["avg_ms_event_timed"]
+    exp = roof["bytes_per_launch"] / (roof["avg_ms"] * 1e-3) / 1e9 / bench.PEAK_HBM_GBS
+    assert math.isclose(roof["frac"], exp, rel_tol=1e-12)
+
+
 def test_c3_rollout_frac_reproduces_from_the_kernel_stats():
     """C3's rollout: ~1.44 KB of reference-layout tuples per hand x 65,536 lanes per launch over
     the launch's 0.09 ms = ~1.05 TB/s, frac ~0.13 -- the same figure from the rocprofv3 average

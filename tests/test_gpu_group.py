@@ -212,3 +212,44 @@ def test_pipelined_group_with_br_partitions_is_deterministic(pkg):
         g.close()
     for x, y in zip(*runs):
         assert np.array_equal(x, y)
+
+
+def test_group_sched_changes_no_sgd_step(pkg):
+    """VERDICT r05 item 7 / ADVICE r05: the group's BR-round and slice schedule is a per-group
+    setting (nfsp_group_set_sched), not process-static environment.  In ONE process, a
+    4-replica pipelined group with the per-slice exchange runs under the default schedule (pieces
+    of <= 40 paced, 2 BR partitions), then under whole segments on one stream, 16-update plain
+    pieces on 4 partitions, and the serial slice loop: nets and counters bit for bit the same
+    (a piece resumes from the weights in memory; the partitions run the same pieces)."""
+    kw = dict(n_lanes=65_536, slices=16, slice_lag=2, rl_capacity=200_000, sl_capacity=400_000)
+    variants = [None, dict(br_cap=0, br_pace=0, br_streams=1), dict(br_cap=16, br_pace=0, br_streams=4),
+                dict(br_cap=40, br_pace=1, br_streams=3), dict(serial=1)]
+    runs = []
+    for v in variants:
+        g = pkg.engine.EngineGroup(4, seed=5151, init_seed=4, **kw)
+        d = g.sched()
+        assert d == dict(br_cap=-1, br_pace=1, br_streams=-1, serial=0), d
+        if v:
+            g.set_sched(**v)
+            assert all(g.sched()[k] == x for k, x in v.items())
+        g.set_exchange(pkg.native.XCHG_AR, every=1, scale=2.0 / 4)
+        g.average_ar()
+        for _ in range(2):
+            g.step()
+        st = [r.stats() for r in g.replicas]
+        assert min(min(s["br_updates"]) for s in st) > 300
+        runs.append(([x.copy() for r in g.replicas for x in nets(r)], st, g.rounds()))
+        g.close()
+    base_nets, base_st, _ = runs[0]
+    for v, (ns, st, _) in zip(variants[1:], runs[1:]):
+        assert st == base_st, v
+        for x, y in zip(base_nets, ns):
+            assert np.array_equal(x, y), v
+    # the schedules differ where they should: whole segments take fewer rounds than 16-pieces
+    assert runs[1][2] < runs[2][2]
+    with pytest.raises(Exception):
+        g2 = pkg.engine.EngineGroup(2, seed=1, init_seed=0, **kw)
+        try:
+            g2.set_sched(br_streams=9)
+        finally:
+            g2.close()

@@ -49,6 +49,12 @@ def test_stubs_cover_what_main_py_uses(pkg):
     import time
     ts = rm.time_stub()
     assert ts.sleep(60) is None and ts.time is time.time and time.sleep is not ts.sleep
+    # only code run with main_builtins gets the stub; sys.modules keeps the real module
+    import sys
+    g = {"__builtins__": rm.main_builtins(ts)}
+    exec("import time\nimport os\ndef f():\n    import time as t\n    return t", g)
+    assert g["time"] is ts and g["f"]() is ts and g["os"] is sys.modules["os"]
+    assert sys.modules["time"] is time
     cp = rm.configparser_stub({("Common", "Episodes"): 7}).ConfigParser()
     cp.read_string("[Common]\nEpisodes: 400000\n[Agent]\nEta: 0.1\n")
     assert cp.get("Common", "Episodes") == "7" and cp.get("Agent", "Eta") == "0.1"
@@ -62,6 +68,10 @@ def test_reference_main_py_runs_unchanged(pkg, capsys, tmp_path):
     out = pkg.reference_main.run(REF_MAIN, episodes=episodes, modules=_oracle_modules(),
                                  plot_to=str(tmp_path / "curve"))
     assert open(REF_MAIN, "rb").read() == before              # nothing edited
+    import sys
+    import time
+    assert out["globals"]["time"].sleep is not time.sleep     # main.py's own sleep is skipped ...
+    assert sys.modules["time"] is time                        # ... and nobody else's
     printed = capsys.readouterr().out
     assert "NFSP by David Joos" in printed                    # main.py:151, its __main__ block ran
     assert out["tf_seeds"] == [1234]                          # main.py:133 with config.ini's Seed
