@@ -18,6 +18,7 @@
 #include "../neural-ficititious-self-play-in-imperfect-information-games_amd/csrc/learner.hip"
 #include "../neural-ficititious-self-play-in-imperfect-information-games_amd/csrc/chain_ar.hip"
 #include "chain_ref.hip"
+#include "../neural-ficititious-self-play-in-imperfect-information-games_amd/csrc/chain8.h"
 
 // the host helpers learner.hip's nfsp_engine_update references (unused here)
 namespace nfsp {
@@ -131,9 +132,22 @@ int main(int argc, char** argv) {
     CK(hipFuncSetAttribute((const void*)k_chain3<1, 0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, CHAIN_LDS));
   }
   const int lds = getenv("CHAIN_LDS_BYTES") ? atoi(getenv("CHAIN_LDS_BYTES")) : CHAIN_LDS;
+  // CHAIN8=1: the 8-wave sample-split chain (chain8.h) instead of k_chain3
+  const bool c8 = getenv("CHAIN8") && atoi(getenv("CHAIN8"));
+  for (const void* f : {(const void*)k_chain8<0, 0, 0>, (const void*)k_chain8<1, 0, 0>,
+                        (const void*)k_chain8<0, 0, 1>, (const void*)k_chain8<1, 0, 1>})
+    CK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, CHAIN_LDS));
   ChainArgs CT = C;
   CT.jobs = djobs;
   auto launch3 = [&]() {
+    if (c8) {
+      if (nblk > 2) {
+        if (relu) k_chain8<1, 0, 1><<<nblk, 512, CHAIN_LDS>>>(CT);
+        else k_chain8<0, 0, 1><<<nblk, 512, CHAIN_LDS>>>(CT);
+      } else if (relu) k_chain8<1, 0><<<nblk, 512, CHAIN_LDS>>>(C);
+      else k_chain8<0, 0><<<nblk, 512, CHAIN_LDS>>>(C);
+      return;
+    }
     if (nblk > 2) {
       if (relu) k_chain3<1, 0, 1><<<nblk, 256, lds>>>(CT);
       else k_chain3<0, 0, 1><<<nblk, 256, lds>>>(CT);
@@ -178,8 +192,8 @@ int main(int argc, char** argv) {
   double cs = 0; for (float v : wout) cs += v;
   unsigned long long hsh = 1469598103934665603ull;     // FNV-1a over the weights' bits
   for (float v : wout) { uint32_t u; memcpy(&u, &v, 4); hsh = (hsh ^ u) * 1099511628211ull; }
-  printf("k_chain3 blocks=%d checksum=%.9g hash=%016llx relu=%d updates=%d sgd_steps=%d  %.3f ms  %.3f us/step  %.2f us/update\n",
-         nblk, cs, hsh, relu, U, steps, ms, ms * 1e3 / steps, ms * 1e3 / U);
+  printf("%s blocks=%d checksum=%.9g hash=%016llx relu=%d updates=%d sgd_steps=%d  %.3f ms  %.3f us/step  %.2f us/update\n",
+         c8 ? "k_chain8" : "k_chain3", nblk, cs, hsh, relu, U, steps, ms, ms * 1e3 / steps, ms * 1e3 / U);
   std::vector<unsigned long long> st(80);
   CK(hipMemcpy(st.data(), dst, 80 * 8, hipMemcpyDeviceToHost));
   const char* names[6] = {"fwd-mfma", "layer2+po", "barrier", "loss+gb2", "bwd+dW1", "update+load"};

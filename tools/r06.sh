@@ -11,5 +11,18 @@ case "$1" in
       "300 python3 -u tools/exploit_curve.py --config c5 --quirks 504 --set slices=16 --set slice_lag=2 --steps 420 --every 20 > $O/kuhn_tb_slices16.jsonl" \
       "300 python3 -u tools/exploit_curve.py --config c5 --set slices=16 --set slice_lag=2 --steps 420 --every 42 > $O/kuhn_ref_slices16.jsonl"
     ;;
+  chain8)       # the 8-wave sample-split chain against k_chain3 (tools/bench_chain.hip)
+    B=tools/bin/bench_chain_${2:-r06c8}_br
+    ./tools/gpu_steps.sh \
+      "60 for r in 1 0; do $B 200 \$r compare; CHAIN8=1 $B 200 \$r compare; CHAIN8=1 $B 2000 \$r compare; done > $O/chain8_compare.log" \
+      "120 for r in 1 0; do for b in 1 2; do $B 2000 \$r time \$b; CHAIN8=1 $B 2000 \$r time \$b; done; done > $O/chain8_time.log"
+    ;;
+  kuhn_lr)      # C5 textbook MSE: lower learning rates against the 0.06-0.09 SGD-noise floor
+    C5="python3 -u tools/exploit_curve.py --config c5 --quirks 504 --set slices=16 --set slice_lag=2 --steps 420 --every 20"
+    ./tools/gpu_steps.sh \
+      "300 $C5 --set lr_ar=0.02 > $O/kuhn_tb_lrar02.jsonl" \
+      "300 $C5 --set lr_ar=0.02 --set lr_br=0.01 > $O/kuhn_tb_lrar02_lrbr01.jsonl" \
+      "300 $C5 --set lr_ar=0.005 > $O/kuhn_tb_lrar005.jsonl"
+    ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
