@@ -161,6 +161,11 @@ __global__ void __launch_bounds__(512) k_chain8(ChainArgs C) {
                                : reinterpret_cast<float*>(&sm.po[w][16 * h + c]) + (g == 0 ? 0 : g == 2 ? 1 : 2);
   const int pw = wv ^ 4;                       // the partner wave (same slice, other half)
   float loss_acc = 0.f;
+#ifdef NFSP_CHAIN_STAMPS
+  unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_last = 0;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
+  const unsigned long long st_t0 = st_last;
+#endif
   auto step = [&](auto PHC) {
     constexpr int PH = decltype(PHC)::value;
     const int slot = PH >= 0 ? PH : (t & 3);
@@ -183,6 +188,7 @@ __global__ void __launch_bounds__(512) k_chain8(ChainArgs C) {
     const floatx4 b2v = lds4(&sm.b2s[wv][0]);
     const floatx4 zh = mfma3t(whi, wmid, wlo, fa);      // Z1^T: hidden 16w + 4g + r, sample 16h + c
     __builtin_amdgcn_sched_barrier(0);
+    CHAIN_STAMP(0);
     // ---- layer 2 partial over the slice (the wave's 16 hidden units)
     float p[3] = {0.f, 0.f, 0.f};
 #pragma unroll
@@ -201,7 +207,9 @@ __global__ void __launch_bounds__(512) k_chain8(ChainArgs C) {
     }
     const floatx4 zs = mfma3(fa, whi, wmid, wlo);       // Z1: sample 16h + 4g + r, hidden 16w + c
     const float4 tg = R.tg[ls];
+    CHAIN_STAMP(1);
     __syncthreads();                                    // B1: the partial outputs
+    CHAIN_STAMP(2);
     const short4x ba0 = tr4(rtr), ba1 = tr4(rtr + 8);
     // ---- output + loss of sample ls (the half's 4 waves redundantly, identical results)
     float d0, d1, d2;
@@ -254,6 +262,7 @@ __global__ void __launch_bounds__(512) k_chain8(ChainArgs C) {
         }
       }
     }
+    CHAIN_STAMP(3);
     // ---- backward, sample-major: samples 16h + 4g + r, hidden 16w + c
     float dz[4];
     float g2_0, g2_1, g2_2;
@@ -292,7 +301,9 @@ __global__ void __launch_bounds__(512) k_chain8(ChainArgs C) {
     sm.xch[wv][0][l] = make_float4(gA[0], gA[1], gA[2], gA[3]);
     sm.xch[wv][1][l] = make_float4(gB[0], gB[1], gB[2], gB[3]);
     sm.xch[wv][2][l] = make_float4(V, U, LsH, 0.f);
+    CHAIN_STAMP(4);
     __syncthreads();                                    // B2: the halves meet
+    CHAIN_STAMP(5);
     const floatx4 pA = lds4(&sm.xch[pw][0][l]);
     const floatx4 pB = lds4(&sm.xch[pw][1][l]);
     const floatx4 pv = lds4(&sm.xch[pw][2][l]);
@@ -319,6 +330,7 @@ __global__ void __launch_bounds__(512) k_chain8(ChainArgs C) {
       }
     }
     stash_slot(PH >= 0 ? ((PH + 2) & 3) : ((t + 2) & 3), va);
+    CHAIN_STAMP(6);
   };
   if (t < T1) {
     {
@@ -346,6 +358,15 @@ __global__ void __launch_bounds__(512) k_chain8(ChainArgs C) {
       for (; t < T1; ++t) step(std::integral_constant<int, -1>{});
     }
   }
+#ifdef NFSP_CHAIN_STAMPS
+  if (l == 0 && C.stamps && blockIdx.x == 0) {
+    unsigned long long t_end;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_end)::"memory");
+    st_acc[8] = t_end - st_t0;
+    st_acc[9] = (unsigned long long)(T1 - (int)(u0 * spu));
+    for (int k = 0; k < 10; ++k) C.stamps[wv * 10 + k] = st_acc[k];
+  }
+#endif
   if (t > (int)(u0 * spu)) {             // the loop ran: W2 / b2 as the last step left them
     const float4 fw = sm.w2t[wv][c];
     W2_0 = fw.x; W2_1 = fw.y; W2_2 = fw.z;

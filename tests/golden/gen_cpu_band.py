@@ -12,6 +12,9 @@ exploitability of the two AR nets as softmax mixed strategies, brute force on th
 GPU evaluator agrees within 1e-5, tests/test_exploit.py).
 
     python tests/golden/gen_cpu_band.py --seeds 8 --hands 32000000 --every 2000000
+    python tests/golden/gen_cpu_band.py --seed0 8 --seeds 16 --out tests/golden/cpu_band_c3mem_s8.json
+    python tests/golden/gen_cpu_band.py --merge tests/golden/cpu_band_c3mem.json \
+        tests/golden/cpu_band_c3mem_s8.json --out tests/golden/cpu_band_c3mem_24.json
 
 Seeds run on host threads (ctypes releases the GIL).  ~4 min on 8 cores.
 """
@@ -47,33 +50,57 @@ def run_seed(s, hands, every, out):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seeds", type=int, default=8)
+    ap.add_argument("--seed0", type=int, default=0, help="first seed (a further sample of seeds)")
+    ap.add_argument("--merge", nargs="+", default=None, help="merge band files (their seeds) into --out")
     ap.add_argument("--hands", type=int, default=32_000_000)
     ap.add_argument("--every", type=int, default=2_000_000)
     ap.add_argument("--out", default=os.path.join(REPO, "tests", "golden", "cpu_band_c3mem.json"))
     args = ap.parse_args()
+    if args.merge:
+        return merge(args.merge, args.out)
     import exploit_oracle as E
     t0 = time.time()
     snaps = {}
-    th = [threading.Thread(target=run_seed, args=(s, args.hands, args.every, snaps)) for s in range(args.seeds)]
+    seeds = list(range(args.seed0, args.seed0 + args.seeds))
+    th = [threading.Thread(target=run_seed, args=(s, args.hands, args.every, snaps)) for s in seeds]
     for t in th:
         t.start()
     for t in th:
         t.join()
     curves = {}
-    for s in range(args.seeds):
+    for s in seeds:
         curves[s] = [(h, float(E.exploitability(w0, w1, 0)["exploitability"])) for h, w0, w1 in snaps[s]]
     by_h = {}
-    for s in range(args.seeds):
+    for s in seeds:
         for h, v in curves[s]:
             by_h.setdefault(h, []).append(v)
     out = {"what": "exact exploitability (softmax mixed, chips) of main.train's AR nets vs hands, "
                    "C++ restatement of the reference (oracle/nfsp_cpu.cpp), C3 memories",
            "generator": "tests/golden/gen_cpu_band.py", "rl_capacity": RL_CAP, "sl_capacity": SL_CAP,
-           "seeds": list(range(args.seeds)), "cpu_seed": "1000 + s", "init_seed": "s",
+           "seeds": seeds, "cpu_seed": "1000 + s", "init_seed": "s",
            "curves_by_hands": {str(h): v for h, v in sorted(by_h.items())},
            "band": {str(h): [float(np.mean(v)), float(np.std(v))] for h, v in sorted(by_h.items())},
            "wall_s": round(time.time() - t0, 1)}
     with open(args.out, "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out["band"]))
+
+
+def merge(paths, out_path):
+    """One band over the seeds of several band files (same memories, same checkpoints)."""
+    ds = [json.load(open(p)) for p in paths]
+    seeds, by_h = [], {}
+    for d in ds:
+        assert (d["rl_capacity"], d["sl_capacity"]) == (ds[0]["rl_capacity"], ds[0]["sl_capacity"])
+        assert not set(seeds) & set(d["seeds"]), "overlapping seeds"
+        seeds += d["seeds"]
+        for h, v in d["curves_by_hands"].items():
+            by_h.setdefault(h, []).extend(v)
+    assert all(len(v) == len(seeds) for v in by_h.values())
+    out = dict(ds[0], seeds=seeds, merged_from=[os.path.relpath(p, REPO) for p in paths],
+               curves_by_hands=by_h, band={h: [float(np.mean(v)), float(np.std(v))] for h, v in by_h.items()},
+               wall_s=sum(d["wall_s"] for d in ds))
+    with open(out_path, "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out["band"]))
 

@@ -196,14 +196,16 @@ int main(int argc, char** argv) {
          c8 ? "k_chain8" : "k_chain3", nblk, cs, hsh, relu, U, steps, ms, ms * 1e3 / steps, ms * 1e3 / U);
   std::vector<unsigned long long> st(80);
   CK(hipMemcpy(st.data(), dst, 80 * 8, hipMemcpyDeviceToHost));
-  const char* names[6] = {"fwd-mfma", "layer2+po", "barrier", "loss+gb2", "bwd+dW1", "update+load"};
-  for (int wv = 0; wv < 4; ++wv) {
+  const char* names3[6] = {"fwd-mfma", "layer2+po", "barrier", "loss+gb2", "bwd+dW1", "update+load"};
+  const char* names8[7] = {"split+zh", "layer2+po", "B1", "loss", "bwd+dW1+xch", "B2", "update"};
+  const int nph = c8 ? 7 : 6, nwv = c8 ? 8 : 4;
+  for (int wv = 0; wv < nwv; ++wv) {
     unsigned long long tot = 0;
-    for (int k = 0; k < 6; ++k) tot += st[wv * 10 + k];
+    for (int k = 0; k < nph; ++k) tot += st[wv * 10 + k];
     if (!tot) continue;
     printf("wave %d cycles/step:", wv);
-    for (int k = 0; k < 6; ++k) printf(" %s=%.0f", names[k], (double)st[wv * 10 + k] / steps);
-    printf("  total=%.0f\n", (double)tot / steps);
+    for (int k = 0; k < nph; ++k) printf(" %s=%.0f", c8 ? names8[k] : names3[k], (double)st[wv * 10 + k] / steps);
+    printf("  total=%.0f kernel=%.0f\n", (double)tot / steps, (double)st[wv * 10 + 8] / steps);
   }
   return 0;
 }

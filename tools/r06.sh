@@ -24,5 +24,21 @@ case "$1" in
       "300 $C5 --set lr_ar=0.02 --set lr_br=0.01 > $O/kuhn_tb_lrar02_lrbr01.jsonl" \
       "300 $C5 --set lr_ar=0.005 > $O/kuhn_tb_lrar005.jsonl"
     ;;
+  kuhn_eps)     # C5 textbook MSE with the reference's decaying epsilon (no NFSP_EXT_EPS_CONST):
+                # a constant 0.06 puts 6 % uniform-random actions into M_SL (one-hot argmax)
+    C5="python3 -u tools/exploit_curve.py --config c5 --set slices=16 --set slice_lag=2 --steps 420 --every 20"
+    ./tools/gpu_steps.sh \
+      "300 $C5 --quirks 440 > $O/kuhn_tb_epsdecay.jsonl" \
+      "300 $C5 --quirks 440 --set lr_ar=0.02 > $O/kuhn_tb_epsdecay_lrar02.jsonl"
+    ;;
+  stamps)
+    B=tools/bin/bench_chain_${2:-r06st}_br
+    ./tools/gpu_steps.sh "120 for r in 1 0; do $B 2000 \$r time; CHAIN8=1 $B 2000 \$r time; done > $O/chain8_stamps.log"
+    ;;
+  c3_seeds)     # C3's learning curve at 16 / 32 / 128 slices over 24 seeds
+    for off in 0 8 16; do
+      ./tools/gpu_steps.sh "600 python3 -u tests/studies/exploit_slices.py --steps 32 --every 8 --variants 16:2 128:2 32:2 --seed-offset $off > $O/c3_slices_seeds$off.json" || exit 1
+    done
+    ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
