@@ -91,6 +91,12 @@ extern "C" {
                        NFSP_EXT_EPS_CONST | NFSP_EXT_SAMPLE_AR)
 /* NFSP_TEXTBOOK with the expected-return (MSE) Q loss: NFSP as Heinrich & Silver train it */
 #define NFSP_TEXTBOOK_MSE (NFSP_TEXTBOOK | NFSP_EXT_MSE_Q)
+/* ... with epsilon decaying as the reference's (eps / iteration) instead of NFSP_EXT_EPS_CONST.
+ * With SL_ONEHOT, a constant 0.06 stores argmax(rand(3)) -- a uniform action -- for 6 % of the
+ * BR decisions, which mixes uniform play into the average policy: Kuhn's exploitability then
+ * stops at 0.06-0.09 chips whatever the learning rates; decaying, it reaches 0.01-0.02
+ * (profiles/r06/kuhn_*.jsonl). */
+#define NFSP_TEXTBOOK_MSE_DECAY (NFSP_TEXTBOOK_MSE & ~NFSP_EXT_EPS_CONST)
 
 typedef struct nfsp_ctx nfsp_ctx;
 

@@ -23,6 +23,7 @@ EXT_SL_ONEHOT, EXT_RESERVOIR, EXT_LINEAR_Q, EXT_EPS_CONST, EXT_SAMPLE_AR = 8, 16
 TEXTBOOK = EXT_SL_ONEHOT | EXT_RESERVOIR | EXT_LINEAR_Q | EXT_EPS_CONST | EXT_SAMPLE_AR
 EXT_MSE_Q = 256
 TEXTBOOK_MSE = TEXTBOOK | EXT_MSE_Q
+TEXTBOOK_MSE_DECAY = TEXTBOOK_MSE & ~EXT_EPS_CONST      # epsilon / iteration, as the reference
 
 P = C.c_void_p
 I32, I64, U32, U64, F32, F64 = C.c_int, C.c_int64, C.c_uint, C.c_uint64, C.c_float, C.c_double

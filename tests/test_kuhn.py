@@ -230,3 +230,25 @@ def test_gpu_kuhn_c5_sliced_reaches_the_plateau_in_a_third_of_the_hands(pkg):
         eng.step()
     e1 = eng.exploitability(0)["exploitability"]
     assert e1 < 0.13, e1
+
+
+@pytest.mark.gpu
+def test_gpu_kuhn_c5_exploitability_below_0_05(pkg):
+    """C5's "exploitability -> 0" (BASELINE configs[4]) at full size: 1,048,576 Kuhn lanes in 16
+    pipelined slices, textbook NFSP with the MSE Q loss and the reference's decaying epsilon
+    (NFSP_TEXTBOOK_MSE_DECAY), lr_ar 0.02.  Measured over 440M hands (profiles/r06/
+    kuhn_tb_epsdecay_lrar02.jsonl): 0.022 at 21M hands, 0.012 at 42M, 0.009-0.016 to 440M.  With
+    a constant epsilon (NFSP_TEXTBOOK_MSE) the curve stops at 0.06-0.09 at every learning rate
+    tried (kuhn_tb_*.jsonl): the epsilon-random BR actions enter M_SL as uniform actions.  The
+    reference algorithm is at 0.68 after 440M (kuhn_ref_slices16.jsonl).  Bar: < 0.05 after 24
+    steps (25M hands)."""
+    nat = pkg.native
+    assert nat.TEXTBOOK_MSE_DECAY == 440
+    eng = pkg.engine.SelfPlayEngine(n_lanes=1_048_576, rl_capacity=200_000, sl_capacity=2_000_000,
+                                    seed=1234, init_seed=0, game=nat.GAME_KUHN, quirks=nat.TEXTBOOK_MSE_DECAY,
+                                    slices=16, slice_lag=2, lr_ar=0.02)
+    e0 = eng.exploitability(0)["exploitability"]
+    for _ in range(24):
+        eng.step()
+    e1 = eng.exploitability(0)["exploitability"]
+    assert e0 > 1.0 and e1 < 0.05, (e0, e1)

@@ -18,7 +18,7 @@
 #include "../neural-ficititious-self-play-in-imperfect-information-games_amd/csrc/learner.hip"
 #include "../neural-ficititious-self-play-in-imperfect-information-games_amd/csrc/chain_ar.hip"
 #include "chain_ref.hip"
-#include "../neural-ficititious-self-play-in-imperfect-information-games_amd/csrc/chain8.h"
+#include "chain8_probe.h"
 
 // the host helpers learner.hip's nfsp_engine_update references (unused here)
 namespace nfsp {

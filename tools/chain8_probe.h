@@ -1,4 +1,12 @@
-// k_chain8: the SGD chain with the minibatch split over two waves per SIMD (round 6).
+// k_chain8: the SGD chain with the minibatch split over two waves per SIMD (round 6) -- a
+// measured experiment, NOT part of libnfsp (tools/bench_chain.hip CHAIN8=1).  Result
+// (profiles/r06/chain8_*.log): correct (200 updates within 1.2e-7 BR / 2.7e-5 AR of the f32
+// reference chain) but SLOWER: 1.016 / 1.091 us per SGD step against k_chain3's 0.719 / 0.758.
+// Its stamps show why: the younger wave of each SIMD pair runs every phase about as long as a
+// k_chain3 wave runs the whole (double) phase, and the older wave waits 250-420 cycles at each
+// barrier for it -- the SIMD's instruction issue, not one wave's, is the bound, and the pair
+// issues ~1.2x k_chain3's instructions per step (the duplicated W split and loss, the
+// exchange).  DESIGN.md Appendix A.0.
 // Reference: agent/agent.py:241-264 (model.fit(batch_size=32, epochs=2) of the BR Q-net and
 // the AR policy net), the same step records and job tables as k_chain3 (chain3.h).
 //
@@ -23,7 +31,7 @@
 // bit-identical to it); every product is still exact (0/1 inputs, exact bf16 splits) and every
 // sum f32.  Parity: the learner tests' written tolerances.
 #pragma once
-#include "chain3.h"
+#include "../neural-ficititious-self-play-in-imperfect-information-games_amd/csrc/chain3.h"
 
 namespace nfsp {
 namespace chain {
