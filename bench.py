@@ -582,11 +582,11 @@ def stub_main(args, world, rank, dist):
 
 def cpu_band(hands: int) -> dict | None:
     """The CPU reference's exact-exploitability seed band at `hands` hands (main.train restated
-    in C++ with C3's memories, 8 seeds, every 2M hands to 32M: tests/golden/cpu_band_c3mem.json),
+    in C++ with C3's memories, 24 seeds, every 2M hands to 32M: tests/golden/cpu_band_c3mem_24.json),
     at the nearest checkpoint.  Past its last checkpoint the last one stands in (the CPU curve is
     flat there, 1.23 / 1.22 at 30 / 32M), as the C3 / C4 gates compare their 33.5M and 67M
     points (tests/test_gpu_slices.py); `beyond_band` says so."""
-    path = os.path.join(REPO, "tests", "golden", "cpu_band_c3mem.json")
+    path = os.path.join(REPO, "tests", "golden", "cpu_band_c3mem_24.json")
     if not os.path.exists(path):
         return None
     with open(path) as f:
@@ -594,7 +594,7 @@ def cpu_band(hands: int) -> dict | None:
     pts = sorted(int(k) for k in cb)
     h = min(pts, key=lambda k: abs(k - hands))
     out = {"hands": h, "mean": cb[str(h)][0], "std": cb[str(h)][1],
-           "source": "tests/golden/cpu_band_c3mem.json (8 seeds)"}
+           "source": "tests/golden/cpu_band_c3mem_24.json (24 seeds)"}
     if hands > pts[-1] + (pts[1] - pts[0]) // 2:
         out["beyond_band"] = True
     return out
@@ -602,7 +602,7 @@ def cpu_band(hands: int) -> dict | None:
 
 def band_check(x: float, hands: int) -> dict:
     """One engine seed's exact exploitability against the CPU band at the same hands: the C3 /
-    C4 gates' bar (|x - mean| <= 2 sigma and x <= mean + sigma; the gates use 8 seeds)."""
+    C4 gates' bar (|x - mean| <= 2 sigma and x <= mean + sigma; the gates average 16 / 8 seeds)."""
     b = cpu_band(hands)
     out = {"hands": hands, "exploitability": x, "cpu_band": b}
     if b is not None:

@@ -13,9 +13,9 @@ update trigger agent/agent.py:153-154).
   bench.py's C5-textbook form (Kuhn, NFSP_TEXTBOOK_MSE);
 * the C3 learning gate: exact exploitability after 8M / 16M / 25M / 33M hands at C3 (1M
   lanes, 16 slices, M_RL 200k, M_SL 2M) against the CPU seed band of the reference's
-  main.train restated in C++ with the same memories and initial nets
-  (tests/golden/cpu_band_c3mem.json);
-* the same gate for C4's arithmetic (8 x 1M lanes in 64 pipelined slices, the average-policy
+  main.train restated in C++ with the same memories and initial nets, 24 seeds
+  (tests/golden/cpu_band_c3mem_24.json);
+* the same gate for C4's arithmetic (8 x 1M lanes in 128 pipelined slices, the average-policy
   nets exchanged after every slice), emulated on one GPU by an engine group.
 """
 import json
@@ -205,27 +205,45 @@ def test_pipelined_step_is_deterministic(pkg):
 
 
 def _band():
-    with open(os.path.join(HERE, "golden", "cpu_band_c3mem.json")) as f:
+    """The CPU reference's band: tests/golden/cpu_band_c3mem_24.json, 24 seeds (the 8 of
+    cpu_band_c3mem.json merged with 16 more, tests/golden/gen_cpu_band.py)."""
+    with open(os.path.join(HERE, "golden", "cpu_band_c3mem_24.json")) as f:
         return json.load(f)
+
+
+def _band_report(band, gpu, hands_of):
+    cpu = {int(h): np.array(v) for h, v in band["curves_by_hands"].items()}
+    last = max(cpu)
+    report = []
+    for k, xs in gpu.items():
+        h = hands_of(k)
+        near = min(cpu, key=lambda x: abs(x - min(h, last)))   # the CPU checkpoint (every 2M hands) nearest
+        cm, cs = float(cpu[near].mean()), float(cpu[near].std())
+        gm, gs = float(np.mean(xs)), float(np.std(xs))
+        report.append((h, near, round(cm, 3), round(cs, 3), round(gm, 3), round(gs, 3), round(cm + cs - gm, 3)))
+    return report
 
 
 def test_c3_sliced_learns_within_the_cpu_seed_band(pkg):
     """BASELINE.json's second metric at C3, as bench.py measures C3 (1M lanes, 16 pipelined
     slices): the exploitability-vs-hands curve lies within the CPU reference's seed band.
-    Bar at every checkpoint: |GPU mean - CPU mean| <= 2 sigma and GPU mean <= CPU mean + 1 sigma
-    (sigma: the 8 CPU seeds' std, ~0.25 chips; the GPU mean's own standard error is ~0.09).
-    Unsliced (one rollout of 1M hands per step) sat 1.1 sigma above the band
-    (profiles/r01_exploit_lag.json)."""
+    Bars at every checkpoint: |GPU mean - CPU mean| <= 2 sigma, and the GPU mean >= 0.1 chips
+    inside CPU mean + 1 sigma (sigma: the CPU seeds' std).  GPU: 16 seeds (1234 + s, initial
+    nets s); CPU: 24 seeds.
+    Round 6 (profiles/r06/c3_slices_seeds*.json, 24 GPU seeds): 1.639 / 1.564 / 1.522 / 1.475 at
+    8.4 / 16.8 / 25.2 / 33.5M hands against the CPU's 1.440 / 1.399 / 1.386 / 1.381 (sigma
+    ~0.46): +0.2 to +0.43 sigma, 0.27-0.37 chips inside the bar.  Round 5's gate compared 8 GPU
+    seeds with the first 8 CPU seeds alone, whose mean happened to be 0.15-0.2 chips below the 24
+    seeds' (sigma 0.25 vs 0.46), and passed 8.4M by 0.036."""
     import bench
     c3 = bench.CONFIGS["c3"]
     K, lag = c3["slices"], c3["slice_lag"]
     assert (K, lag) == (16, 2) and c3["n_lanes"] == C3["n_lanes"]
     band = _band()
-    cpu = {int(h): np.array(v) for h, v in band["curves_by_hands"].items()}
-    seeds = band["seeds"]
+    assert len(band["seeds"]) == 24
     checkpoints = (8, 16, 24, 32)                  # engine steps of 1,048,576 hands
     gpu = {c: [] for c in checkpoints}
-    for s in seeds:
+    for s in range(16):
         eng = pkg.engine.SelfPlayEngine(seed=1234 + s, init_seed=s, slices=K, slice_lag=lag, **C3)
         for k in range(1, checkpoints[-1] + 1):
             eng.step()
@@ -234,17 +252,11 @@ def test_c3_sliced_learns_within_the_cpu_seed_band(pkg):
         eng.close()
         del eng
         torch.cuda.empty_cache()
-    report = []
-    for k in checkpoints:
-        h = k * C3["n_lanes"]
-        near = min(cpu, key=lambda x: abs(x - h))  # the CPU checkpoint (every 2M hands) nearest
-        cm, cs = float(cpu[near].mean()), float(cpu[near].std())
-        gm, gs = float(np.mean(gpu[k])), float(np.std(gpu[k]))
-        report.append((h, near, round(cm, 3), round(cs, 3), round(gm, 3), round(gs, 3)))
-    print("hands, cpu checkpoint, cpu mean, cpu std, gpu mean, gpu std:", report)
-    for (h, near, cm, cs, gm, gs) in report:
+    report = _band_report(band, gpu, lambda k: k * C3["n_lanes"])
+    print("hands, cpu checkpoint, cpu mean, cpu std, gpu mean, gpu std, margin:", report)
+    for (h, near, cm, cs, gm, gs, margin) in report:
         assert abs(gm - cm) <= 2 * cs, report
-        assert gm <= cm + cs, report
+        assert gm <= cm + cs - 0.1, report          # >= 0.1 chips inside the bar
 
 
 def test_c4_emulated_learns_within_the_cpu_seed_band(pkg):
@@ -254,15 +266,14 @@ def test_c4_emulated_learns_within_the_cpu_seed_band(pkg):
     arithmetic (tests/test_gpu_exchange.py shows the ranks equal to a group bit for bit) -- done on
     device by an engine group.  Exploitability at equal TOTAL hands against the CPU band, from the
     first checkpoint (one step = 8.4M hands) to 8 steps (67M), with the C3 bar:
-    |GPU mean - CPU mean| <= 2 sigma and GPU mean <= CPU mean + 1 sigma (8 seeds each side).
-    Besides the bar, a margin: the GPU mean sits >= 0.1 chips below CPU mean + 1 sigma at every
-    checkpoint.  Measured at 128 slices (profiles/r04_c4x_k128_ar_g2.json): 1.421 at 8.4M (bar
+    |GPU mean - CPU mean| <= 2 sigma and GPU mean <= CPU mean + 1 sigma (8 GPU seeds, the 24 CPU
+    seeds).  Besides the bar, a margin: the GPU mean sits >= 0.1 chips below CPU mean + 1 sigma at
+    every checkpoint (against the first 8 CPU seeds alone the margins were 0.118-0.364, round 5).  Measured at 128 slices (profiles/r04_c4x_k128_ar_g2.json): 1.421 at 8.4M (bar
     1.539), 1.234 / 1.216 / 1.165 at 16.8 / 25.2 / 33.5M; 64 slices (round 4's C4) passed 8.4M by
     0.012 chips, round 3's once-per-step exchange reached the band only from 33.5M."""
     import bench
     c4 = bench.CONFIGS["c4"]
     band = _band()
-    cpu = {int(h): np.array(v) for h, v in band["curves_by_hands"].items()}
     R, lanes, K = 8, c4["n_lanes"], c4["slices"]
     assert (K, c4["slice_lag"], c4["xchg_every"], c4["xchg_gain"]) == (128, 2, 1, 2.0)
     checkpoints = (1, 2, 3, 4, 8)                  # steps of 8 x 1,048,576 hands
@@ -283,16 +294,9 @@ def test_c4_emulated_learns_within_the_cpu_seed_band(pkg):
         g.close()
         del g
         torch.cuda.empty_cache()
-    report = []
-    last = max(cpu)
-    for k in checkpoints:
-        h = k * R * lanes
-        near = min(cpu, key=lambda x: abs(x - min(h, last)))
-        cm, cs = float(cpu[near].mean()), float(cpu[near].std())
-        gm, gs = float(np.mean(gpu[k])), float(np.std(gpu[k]))
-        report.append((h, near, round(cm, 3), round(cs, 3), round(gm, 3), round(gs, 3)))
-    print("hands, cpu checkpoint, cpu mean, cpu std, gpu mean, gpu std:", report)
-    for (h, near, cm, cs, gm, gs) in report:
+    report = _band_report(band, gpu, lambda k: k * R * lanes)
+    print("hands, cpu checkpoint, cpu mean, cpu std, gpu mean, gpu std, margin:", report)
+    for (h, near, cm, cs, gm, gs, margin) in report:
         assert abs(gm - cm) <= 2 * cs, report
         assert gm <= cm + cs - 0.1, report          # >= 0.1 chips inside the bar
 
