@@ -40,20 +40,14 @@ case "$1" in
       ./tools/gpu_steps.sh "600 python3 -u tests/studies/exploit_slices.py --steps 32 --every 8 --variants 16:2 128:2 32:2 --seed-offset $off > $O/c3_slices_seeds$off.json" || exit 1
     done
     ;;
-  persist)      # k_br_persist's hand-off protocol and geometry, trivial work
+  persist)      # k_br_persist's hand-off protocol and geometry, trivial work.
+                # One timeout ends the call (tools/gpu_steps.sh), so the expected-good runs go first.
+    P=tools/bin/persist_probe
     ./tools/gpu_steps.sh \
-      "60 tools/bin/persist_probe 1 3 150 2000 0 > $O/persist_probe_r1.log" \
-      "60 tools/bin/persist_probe 2 3 150 2000 0 > $O/persist_probe_r2.log" \
-      "60 tools/bin/persist_probe 16 4 150 2000 0 > $O/persist_probe_r16.log" \
-      "60 tools/bin/persist_probe 2 3 150 2000 1 > $O/persist_probe_r2_slow.log"
-    ;;
-  c3_fine)      # finer slices: learning (16 seeds) and throughput at 256 / 512 / 1024 slices
-    for k in 16 128 256 512 1024; do
-      ./tools/gpu_steps.sh "300 python3 -u bench.py --config c3 --slices $k --no-cpu --groups '' --steps 10 --warmup 3 > $O/c3_bench_slices$k.json" || exit 1
-    done
-    for off in 0 8; do
-      ./tools/gpu_steps.sh "600 python3 -u tests/studies/exploit_slices.py --steps 32 --every 8 --variants 256:2 512:2 1024:2 --seed-offset $off > $O/c3_fine_seeds$off.json" || exit 1
-    done
+      "20 $P 1 3 150 1048576 0 16384 > $O/persist_small_lds.log" \
+      "20 $P 1 3 150 1048576 0 > $O/persist_big_lds.log" \
+      "20 $P 1 3 150 2000 0 16384 > $O/persist_small_lds_bails.log" \
+      "20 $P 1 3 150 2000 0 > $O/persist_big_lds_bails.log"
     ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
