@@ -49,5 +49,20 @@ case "$1" in
       "20 $P 1 3 150 2000 0 16384 > $O/persist_small_lds_bails.log" \
       "20 $P 1 3 150 2000 0 > $O/persist_big_lds_bails.log"
     ;;
+  final)        # the committed tree: the GPU suite, smoke(), the driver's bench command
+    ./tools/gpu_steps.sh \
+      "900 python3 -u -m pytest tests -m gpu -v --durations=15 --timeout 400 --timeout-method thread > $O/gputest_final.log" \
+      "300 python3 -u -c 'import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")' > $O/smoke_final.log" \
+      "600 python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_final.json"
+    ;;
+  prof)         # rocprofv3 --kernel-trace --stats of the driver's command, then the PMC passes
+    R=$(pwd); D=$R/$O/prof; mkdir -p $D
+    ( cd /tmp && export TMPDIR=/tmp &&
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o drv -- python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 > $D/bench.json 2> $D/bench.err &&
+      timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $D -o pmc_fetch -- python3 $R/bench.py --config c3 --no-cpu --groups '' > $D/pmc_fetch.json 2> $D/pmc_fetch.err &&
+      timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $D -o pmc_write -- python3 $R/bench.py --config c3 --no-cpu --groups '' > $D/pmc_write.json 2> $D/pmc_write.err ) || { tail -20 $D/*.err; exit 1; }
+    python3 tools/pmc_summary.py $D c3 > $O/pmc_c3_r06.json
+    find $D -name "*stats*"
+    ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
