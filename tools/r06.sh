@@ -42,10 +42,15 @@ case "$1" in
     ;;
   persist)      # k_br_persist's hand-off protocol and geometry, trivial work.
                 # A host watchdog prints the kernel's progress counters and exits after 10 s.
+                # The variant that compiles a device printf in goes last.
     P=tools/bin/persist_probe
     ./tools/gpu_steps.sh \
-      "20 $P 1 3 150 1048576 4 16384 > $O/persist_sanity.log" \
-      "20 $P 1 3 150 1048576 0 16384 > $O/persist_small_lds.log"
+      "20 $P 1 3 150 1048576 0 > $O/persist_big_lds.log" \
+      "20 $P 2 3 150 1048576 0 > $O/persist_r2.log" \
+      "20 $P 16 4 150 1048576 0 > $O/persist_r16.log" \
+      "20 $P 2 3 150 2000 1 > $O/persist_r2_slow_bails.log" \
+      "20 $P 2 3 150 1048576 16 > $O/persist_r2_devmem.log" \
+      "20 $P 2 3 150 1048576 8 > $O/persist_r2_printf.log"
     ;;
   final)        # the committed tree: the GPU suite, smoke(), the driver's bench command
     ./tools/gpu_steps.sh \
