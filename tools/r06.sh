@@ -42,7 +42,6 @@ case "$1" in
     ;;
   persist)      # k_br_persist's hand-off protocol and geometry, trivial work.
                 # A host watchdog prints the kernel's progress counters and exits after 10 s.
-                # The variant that compiles a device printf in goes last.
     P=tools/bin/persist_probe
     ./tools/gpu_steps.sh \
       "20 $P 1 3 150 1048576 0 > $O/persist_big_lds.log" \
@@ -51,6 +50,14 @@ case "$1" in
       "20 $P 2 3 150 2000 1 > $O/persist_r2_slow_bails.log" \
       "20 $P 2 3 150 1048576 16 > $O/persist_r2_devmem.log" \
       "20 $P 2 3 150 1048576 8 > $O/persist_r2_printf.log"
+    ;;
+  persist2)     # the first probes' exact host / atomics configuration, one factor at a time
+    P=tools/bin/persist_probe
+    ./tools/gpu_steps.sh \
+      "20 $P 1 3 150 1048576 48 16384 > $O/persist2_sync_devmem.log" \
+      "20 $P 1 3 150 1048576 112 16384 > $O/persist2_sync_devmem_agent.log" \
+      "20 $P 1 3 150 1048576 120 16384 > $O/persist2_sync_devmem_agent_printf.log" \
+      "20 $P 1 3 150 2000 120 > $O/persist2_v1.log"
     ;;
   final)        # the committed tree: the GPU suite, smoke(), the driver's bench command
     ./tools/gpu_steps.sh \
