@@ -584,7 +584,7 @@ def cpu_band(hands: int) -> dict | None:
     """The CPU reference's exact-exploitability seed band at `hands` hands (main.train restated
     in C++ with C3's memories, 24 seeds, every 2M hands to 32M: tests/golden/cpu_band_c3mem_24.json),
     at the nearest checkpoint.  Past its last checkpoint the last one stands in (the CPU curve is
-    flat there, 1.23 / 1.22 at 30 / 32M), as the C3 / C4 gates compare their 33.5M and 67M
+    flat there, 1.384 / 1.381 at 30 / 32M), as the C3 / C4 gates compare their 33.5M and 67M
     points (tests/test_gpu_slices.py); `beyond_band` says so."""
     path = os.path.join(REPO, "tests", "golden", "cpu_band_c3mem_24.json")
     if not os.path.exists(path):

@@ -74,5 +74,9 @@ case "$1" in
     python3 tools/pmc_summary.py $D c3 > $O/pmc_c3_r06.json
     find $D -name "*stats*"
     ;;
+  all)          # the final validation, the profiles, then the persist probe variants (last: a
+                # variant may hang, and a timeout ends the call)
+    ./tools/r06.sh final && ./tools/r06.sh prof && ./tools/r06.sh persist2
+    ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
