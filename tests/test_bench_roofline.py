@@ -13,7 +13,7 @@ import pytest
 
 from conftest import REPO
 
-PROFILES = [("r05_bench_driver_cmd.json", "c3"), ("r04_bench_measure.json", "c3"), ("r03_bench_default.json", "c3"), ("r03_c2_bench.json", "c2"),
+PROFILES = [("r06_driver_cmd_prof_bench.json", "c3"), ("r05_bench_driver_cmd.json", "c3"), ("r04_bench_measure.json", "c3"), ("r03_bench_default.json", "c3"), ("r03_c2_bench.json", "c2"),
             ("r03_c5_bench.json", "c5"), ("r03_c5_tb_bench.json", "c5_tb")]
 
 
@@ -99,7 +99,8 @@ def test_c3_rollout_frac_reproduces_from_the_kernel_stats():
 
 @pytest.mark.parametrize("line,stats", [("r04_bench_measure.json", "r04_c3_kernel_stats.csv"),
                                         ("r04_driver_cmd_prof_bench.json", "r04_driver_cmd_kernel_stats.csv"),
-                                        ("r05_driver_cmd_prof_bench.json", "r05_driver_cmd_kernel_stats.csv")])
+                                        ("r05_driver_cmd_prof_bench.json", "r05_driver_cmd_kernel_stats.csv"),
+                                        ("r06_driver_cmd_prof_bench.json", "r06_driver_cmd_kernel_stats.csv")])
 def test_c3_dominant_chain_duration_agrees_with_rocprof(line, stats):
     """The headline's roofline kernel (the chain on the critical stream) has the same average
     launch duration in bench's live HIP-event pass and in the rocprofv3 kernel statistics of the
@@ -134,3 +135,20 @@ def test_cpu_band_lookup_matches_the_learning_gates():
         assert b["hands"] == 32_000_000 and b["beyond_band"] is True
     c = bench.band_check(1.0, 33_554_432)
     assert c["inside_bar"] is True and c["cpu_band"]["beyond_band"] is True
+
+
+def test_r06_line_frac_matches_rocprof_within_one_percent():
+    """VERDICT r05 item 4's acceptance on the round-6 tree: the driver's command under rocprofv3
+    (profiles/r06_driver_cmd_prof_bench.json) reports a roofline whose avg_ms comes from the
+    un-instrumented step, never exceeds the step, and whose frac matches the rocprofv3 average
+    of the same kernel in the same run (r06_driver_cmd_kernel_stats.csv) within 1 %."""
+    import csv
+    with open(os.path.join(REPO, "profiles", "r06_driver_cmd_prof_bench.json")) as f:
+        d = json.load(f)
+    roof = d["roofline"]
+    assert roof["launches_per_step"] * roof["avg_ms"] <= d["ms_per_step"] * 1.005
+    with open(os.path.join(REPO, "profiles", "r06_driver_cmd_kernel_stats.csv")) as f:
+        rows = [row for row in csv.DictReader(f) if "k_chain3<0, 0, 0>" in row["Name"]]
+    avg_ms = float(rows[0]["AverageNs"]) * 1e-6
+    frac_rocprof = roof["bytes_per_launch"] / (avg_ms * 1e-3) / 1e9 / roof["peak"]
+    assert abs(frac_rocprof - roof["frac"]) <= 0.01 * roof["frac"], (frac_rocprof, roof["frac"])
