@@ -322,6 +322,39 @@ def init_dist(backend=None, force: bool = False):
     return world, rank, local, dist
 
 
+class StepWatchdog:
+    """N > 1: a rank whose step makes no progress for `limit_s` (env NFSP_STEP_WATCHDOG_S,
+    default 600) exits with 124 after saying where it is.  The per-slice AR exchange is an RCCL
+    all-reduce that libnfsp enqueues on its own stream, outside torch's process-group timeout: a
+    rank whose peer died or never joined would otherwise wait on the device forever, and with it
+    the job.  Exiting lets the launcher (torch.distributed.run, or launch_ranks) stop the others.
+    `beat(what)` marks progress; a daemon thread checks every second."""
+
+    def __init__(self, rank: int, limit_s: float | None = None):
+        import threading
+        self.rank = rank
+        self.limit_s = float(os.environ.get("NFSP_STEP_WATCHDOG_S", "600")) if limit_s is None else limit_s
+        self.what, self.t = "start", time.monotonic()
+        self._stop = threading.Event()
+        self._th = threading.Thread(target=self._run, daemon=True)
+        self._th.start()
+
+    def beat(self, what: str):
+        self.what, self.t = what, time.monotonic()
+
+    def _run(self):
+        while not self._stop.wait(1.0):
+            idle = time.monotonic() - self.t
+            if idle > self.limit_s:
+                sys.stderr.write(f"bench.py: rank {self.rank} made no progress for {idle:.0f} s (last: "
+                                 f"{self.what}); exiting so the launcher stops the job\n")
+                sys.stderr.flush()
+                os._exit(124)
+
+    def stop(self):
+        self._stop.set()
+
+
 def timed_steps(step, steps, warmup, dist=None, sync=lambda: None, device="cuda", out=None):
     """W untimed warmup steps, then exactly K timed steps bracketed by a barrier + device
     sync on both sides; returns the MAX elapsed seconds over ranks (every rank gets it).
@@ -533,8 +566,17 @@ def stub_main(args, world, rank, dist):
             fallback = "rccl setup failed on some rank: stub"
         refuse_host_fallback(args, world, fallback)
     gen = torch.Generator().manual_seed(rank)
+    wd = StepWatchdog(rank) if dist is not None and world > 1 else None
+    hang = tuple(int(v) for v in args.stub_hang.split(":")) if args.stub_hang else None
+    nstep = [0]
 
     def step():
+        nstep[0] += 1
+        if wd is not None:
+            wd.beat(f"step {nstep[0]}")
+        if hang is not None and rank == hang[0] and nstep[0] == hang[1]:
+            while True:                      # a rank stuck as in an all-reduce whose peer is gone
+                time.sleep(1.0)
         for _ in range(slices):
             if xchg:
                 d = torch.rand(net.numel(), generator=gen) * 1e-3
@@ -850,6 +892,8 @@ def main():
     ap.add_argument("--stub-diverge", type=int, default=None, help=argparse.SUPPRESS)
     # test hook with --stub-step-ms: rank R exits with code C after the process group is up
     ap.add_argument("--stub-fail", default=None, help=argparse.SUPPRESS)
+    # test hook with --stub-step-ms: rank R's step N never returns (a peer lost in a collective)
+    ap.add_argument("--stub-hang", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--slices", type=int, default=None, help="override the config's lane slices")
     ap.add_argument("--slice-lag", type=int, default=None, choices=[1, 2],
                     help="override the config's slice lag (2: slices pipelined)")
@@ -887,6 +931,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local % torch.cuda.device_count())   # one rank per GPU (mod: rehearsals)
     world, rank, local, dist = init_dist(args.dist_backend, force=args.ar_allreduce == "on")
+    # N > 1: a rank stuck on the device (an RCCL exchange or communicator setup whose peer is
+    # gone) exits instead of holding the job until the driver's limit
+    wd = StepWatchdog(rank) if dist is not None and world > 1 else None
 
     import __graft_entry__
     pkg = __graft_entry__.load_package()
@@ -910,11 +957,18 @@ def main():
     if R == 1 and dist is not None and (args.ar_allreduce == "on" or (args.ar_allreduce == "auto" and world > 1)):
         # C4: the AR nets of both agents, W0 + mean of the ranks' deltas after every
         # `xchg_every`-th slice, on the AR chain stream
+        if wd is not None:
+            wd.beat("exchange setup (RCCL communicator)")
         avg = pkg.shards.AvgPolicyExchange(eng, dist, every=args.xchg_every, transport=args.xchg_transport,
                                            gain=args.xchg_gain)
         refuse_host_fallback(args, world, avg.fallback)
 
+    nstep = [0]
+
     def step():
+        nstep[0] += 1
+        if wd is not None:
+            wd.beat(f"engine step {nstep[0]}")
         eng.step()
     dev = "cuda" if args.dist_backend == "nccl" else "cpu"
     for _ in range(args.warmup):

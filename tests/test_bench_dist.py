@@ -191,3 +191,18 @@ def test_diverged_ar_nets_end_the_job():
                              "--config", "c2", "--stub-diverge", "1"])
     assert rc == 2 and not lines, err
     assert "AR nets differ over the ranks after the timed pass" in err
+
+
+def test_stuck_rank_ends_the_job():
+    """a rank stuck in a step (here: rank 1's second step never returns, as in
+    an exchange whose peer is gone -- libnfsp's RCCL all-reduce is outside torch's process-group
+    timeout) exits 124 once its step watchdog (NFSP_STEP_WATCHDOG_S) sees no progress, and the
+    launcher stops the other rank: the job ends with 124 in seconds, with no result line."""
+    t0 = time.time()
+    rc, lines, err = _bench(["--gpus", "2", "--steps", "4", "--warmup", "1", "--stub-step-ms", "5",
+                             "--config", "c2", "--stub-hang", "1:2"],
+                            env_extra={"NFSP_STEP_WATCHDOG_S": "3", "NFSP_PG_TIMEOUT_S": "600"})
+    assert rc == 124, err
+    assert not lines
+    assert "rank 1 made no progress" in err and "last: step 2" in err
+    assert time.time() - t0 < 60
