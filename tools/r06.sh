@@ -78,5 +78,9 @@ case "$1" in
                 # variant may hang, and a timeout ends the call)
     ./tools/r06.sh final && ./tools/r06.sh prof && ./tools/r06.sh persist2
     ;;
+  c4w1)         # C4's per-rank line with the RCCL exchange at world 1, on the final bench.py
+    ./tools/gpu_steps.sh \
+      "300 python3 -u bench.py --config c4 --ar-allreduce on --no-cpu --groups '' --steps 10 --warmup 3 > $O/c4_rank_xchg_world1.json"
+    ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
