@@ -82,5 +82,10 @@ case "$1" in
     ./tools/gpu_steps.sh \
       "300 python3 -u bench.py --config c4 --ar-allreduce on --no-cpu --groups '' --steps 10 --warmup 3 > $O/c4_rank_xchg_world1.json"
     ;;
+  more_seeds)   # C4's emulation over 16 more seeds; C3 to 134M hands over 8 seeds
+    ./tools/gpu_steps.sh \
+      "600 python3 -u tests/studies/c4_gate_seeds.py --seeds 8 24 > $O/c4_gate_seeds8_23.json" \
+      "600 python3 -u tests/studies/exploit_slices.py --steps 128 --every 16 --variants 16:2 > $O/c3_long_128steps.json"
+    ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
