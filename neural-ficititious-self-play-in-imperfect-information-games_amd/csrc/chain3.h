@@ -95,6 +95,9 @@ constexpr unsigned PK_L2 = 1, PK_O = 2, PK_W = 4, PK_SM = 8;
 #endif
 template <int RELU>
 constexpr unsigned chain_pk() { return RELU == 0 ? (NFSP_PK_AR) : (NFSP_PK_BR); }
+#ifndef NFSP_CHAIN_G0ROW
+#define NFSP_CHAIN_G0ROW 0
+#endif
 
 __device__ inline float dpp_f(float x, int ctrl) {
   switch (ctrl) {   // the control word must be an immediate
@@ -441,7 +444,10 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
   //   is 4 gb2[0], scaled by 1/4 -- exact)        rows 0, 1: b2[1]   rows 2, 3: b2[2]  (own2)
   float* const own1 = g == 3 ? &sm.b2s[w][0] : reinterpret_cast<float*>(&sm.w2t[w][c]) + (g == 0 ? 0 : g == 1 ? 2 : 1);
   float* const own2 = &sm.b2s[w][g < 2 ? 1 : 2];
-  const float own1_sc = g == 3 ? 0.25f : 1.0f;
+  // NFSP_CHAIN_G0ROW (round 6): gb2[0] enters the V transpose as each row's own 16-sample sum
+  // (tot_rows) instead of the 32-sample total replicated in every lane (tot32: one permlane32 and
+  // a copy more); rows g and g ^ 1 hold the same 16 samples, so row 3's total is 2 gb2[0]
+  const float own1_sc = g == 3 ? (NFSP_CHAIN_G0ROW ? 0.5f : 0.25f) : 1.0f;
 #ifdef NFSP_CHAIN_STAMPS
   unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_last = 0;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
@@ -650,7 +656,7 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
     }
     // gb2 = the 32-sample sums of d (round-3 order): gb2[0] in every lane, gb2[1] in rows 0 / 1
     // and gb2[2] in rows 2 / 3 (U, the rows that own b2[1] / b2[2])
-    const float G0 = tot32(d0);
+    const float G0 = NFSP_CHAIN_G0ROW ? tot_rows(d0) : tot32(d0);
     const float U = tot32_pair(d1, d2);
     CHAIN_STAMP(3);
     // ---- backward in the sample-major layout: samples 16 mt + 4g + r, hidden 16w + c

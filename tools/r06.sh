@@ -87,5 +87,11 @@ case "$1" in
       "600 python3 -u tests/studies/c4_gate_seeds.py --seeds 8 24 > $O/c4_gate_seeds8_23.json" \
       "600 python3 -u tests/studies/exploit_slices.py --steps 128 --every 16 --variants 16:2 > $O/c3_long_128steps.json"
     ;;
+  chain_ab)     # A/B of two chain microbenchmark builds: tools/r06.sh chain_ab <tagA> <tagB>
+    A=tools/bin/bench_chain_$2_br; B=tools/bin/bench_chain_$3_br
+    ./tools/gpu_steps.sh \
+      "60 for r in 1 0; do $A 200 \$r compare; $B 200 \$r compare; done > $O/chain_ab_$2_$3_compare.log" \
+      "200 for i in 1 2 3; do for r in 1 0; do $A 2000 \$r time; $B 2000 \$r time; done; done > $O/chain_ab_$2_$3_time.log"
+    ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
