@@ -95,6 +95,14 @@ constexpr unsigned PK_L2 = 1, PK_O = 2, PK_W = 4, PK_SM = 8;
 #endif
 template <int RELU>
 constexpr unsigned chain_pk() { return RELU == 0 ? (NFSP_PK_AR) : (NFSP_PK_BR); }
+// NFSP_CHAIN_G0ROW: gb2[0] enters the V transpose as each lane row's 16-sample sum instead of
+// the 32-sample total (see own1_sc).  Measured in round 6 and left off: tools/r06.sh chain_ab
+// gave AR 0.760 -> 0.750 us per SGD step but BR 0.721 -> 0.727; built into the AR chain only,
+// the driver's bench read 7.02M hands/s (7.09M without) and the Leduc learner parity case with
+// the textbook extensions (quirks 120) moved to 2.1e-3 against its 1e-3 bound (a ReLU crossing
+// follows the new summation order).  Also measured and dropped: the BR loss without relu(o)
+// in e and with -1 / (3 x batch) folded into the rate, 5 instructions fewer per step but
+// 0.721 -> 0.736 (the schedule moved).
 #ifndef NFSP_CHAIN_G0ROW
 #define NFSP_CHAIN_G0ROW 0
 #endif
