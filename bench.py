@@ -115,6 +115,13 @@ CONFIGS = {
                                    f"slices each), M_RL 200k + M_SL 2M each, reference cadence; the replicas' AR "
                                    f"nets exchanged after every slice (W0 + 2 x mean delta), from scratch")
        for R in (4, 8)},
+    # the same with the group's BR learner call as one persistent launch (nfsp_group_sched
+    # br_persist, k_br_persist: DESIGN.md Appendix A.1b) -- the same SGD steps bit for bit
+    "c4_emul_r8_persist": dict(n_lanes=8 * 1_048_576, replicas=8, slices=128, slice_lag=2, rl_capacity=200_000,
+                               sl_capacity=2_000_000, xchg_every=1, xchg_gain=2.0, learn_steps=4,
+                               sched=dict(br_persist=1),
+                               label="C4 emulated on one GPU as c4_emul_r8, the BR learner calls as one persistent "
+                                     "launch each (k_br_persist)"),
     "c5": dict(n_lanes=1_048_576, slices=16, slice_lag=2, rl_capacity=200_000, sl_capacity=2_000_000,
                game="kuhn", label="C5: Kuhn swap-in, 1,048,576 lanes/GPU (16 pipelined slices), C3's "
                                   "memories and cadence"),
@@ -684,7 +691,9 @@ def measure_group(pkg, name: str, steps: int, warmup: int) -> dict:
     extra = {k: cfg[k] for k in ("slices", "slice_lag") if k in cfg}
     g = pkg.engine.EngineGroup(R, n_lanes=lanes, rl_capacity=cfg["rl_capacity"], sl_capacity=cfg["sl_capacity"],
                                seed=1234, init_seed=0, avg_ar=not xchg, **extra)
-    out = {"workload": cfg["label"], "learner_replicas": R, "lanes_per_replica": lanes,
+    if cfg.get("sched"):
+        g.set_sched(**cfg["sched"])
+    out = {"workload": cfg["label"], "learner_replicas": R, "lanes_per_replica": lanes, "sched": g.sched(),
            "metric": "hands/s (beside it RL inserts/s: M_RL inserts, each 1/128 of an update_strategy)",
            "unit": "hands/s"}
     s0 = g.stats()
@@ -709,6 +718,7 @@ def measure_group(pkg, name: str, steps: int, warmup: int) -> dict:
         torch.cuda.synchronize()
         s0 = g.stats()
         el = timed_steps(g.step, steps, 0, None, torch.cuda.synchronize)
+    g.check()                                    # (a persistent BR kernel's expired wait raises)
     s1 = g.stats()
     hands = steps * cfg["n_lanes"]
     rl = sum(s1["rl_total"]) - sum(s0["rl_total"])

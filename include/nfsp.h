@@ -462,11 +462,18 @@ int nfsp_group_set_exchange(nfsp_group* g, unsigned nets, int every, float scale
  *   br_streams  BR partitions, each its own rounds on its own stream (1..4); -1: 2 for sliced
  *               groups, else 1 (always 1 when chains share CUs)
  *   serial      1: the slices of a pipelined group run one after another (no overlap)
+ *   br_persist  0: BR rounds.  >= 1: a learner call's BR work in ONE launch of the persistent
+ *               kernel k_br_persist -- a chain workgroup per (replica, agent) and 48 helper
+ *               workgroups writing the targets from a device work queue (groups of <= 32
+ *               replicas, the reference's BR net, no loss log; others keep the rounds).  Values
+ *               > 1 bound every device wait at that many s_sleep 8 rounds (default 2^18); an
+ *               expired wait ends the kernel and the error surfaces at the next learner call or
+ *               nfsp_group_check.  br_cap / br_pace / br_streams do not apply to it.
  * nfsp_group_default_sched reads the environment's NFSP_GROUP_BR_CAP / _BR_PACE / _BR_STREAMS /
- * NFSP_GROUP_SERIAL at that call (nfsp_group_create starts from it); nfsp_group_set_sched
- * applies from the next learner call. */
+ * NFSP_GROUP_SERIAL / NFSP_GROUP_BR_PERSIST at that call (nfsp_group_create starts from it);
+ * nfsp_group_set_sched applies from the next learner call. */
 typedef struct nfsp_group_sched {
-  int32_t br_cap, br_pace, br_streams, serial;
+  int32_t br_cap, br_pace, br_streams, serial, br_persist;
 } nfsp_group_sched;
 int nfsp_group_default_sched(nfsp_group_sched* out);
 int nfsp_group_set_sched(nfsp_group* g, const nfsp_group_sched* sched);
@@ -480,6 +487,8 @@ int nfsp_group_get_timings(nfsp_group* g, double* ms /*[NFSP_TIMING_SLOTS]*/,
  * replicas' BR jobs into 2 partitions (nfsp_group_sched.br_streams, 1..4), each with its own
  * rounds on its own stream; the SGD steps are the same as with one. */
 int nfsp_group_rounds(nfsp_group* g, int64_t* out);
+/* Synchronise the group's streams and report a k_br_persist wait that expired (NFSP_EHIP). */
+int nfsp_group_check(nfsp_group* g);
 /* Diagnostic trace of the learner calls' plans (tools/c4_slice_spread.py: the lockstep cost of
  * a per-slice exchange across C4 ranks).  on = 1 clears and starts it; every learner call then
  * appends, per replica r and agent a, its AR and BR update counts: [call][r][a][AR, BR].

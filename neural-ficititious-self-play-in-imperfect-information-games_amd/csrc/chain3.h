@@ -373,428 +373,14 @@ __global__ void __launch_bounds__(256) k_chain3(ChainArgs C) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   Chain3Smem& sm = *reinterpret_cast<Chain3Smem*>(smem_raw);
   const ChainJob J = TABLE ? C.jobs[blockIdx.x] : C.job[blockIdx.x];
-  // the loss-log build (a diagnostic, tests/test_gpu_nn / observability) runs the scalar forms:
-  // its extra loss code put packed writes near MFMA registers (tools/mfma_hazards.py rule 2);
-  // the packed forms round exactly as the scalar ones, so its weights are the same either way
-  constexpr unsigned PK = LOSS ? 0u : chain_pk<RELU>();
-  const int tid = threadIdx.x;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int l = tid & 63;
-  const int g = l >> 4, c = l & 15;
-  const int hid = 16 * w + c;
-  const int sl = 16 * (g >> 1) + c;            // this lane's layer-2 partial sample (Z1^T)
-  // this lane's loss sample: lane j < 8 of row g holds sample 4g + (j & 3) + 16 (j >> 2), the
-  // samples the row's backward slot j needs (bwd_dpp); lanes 8..15 hold the other row of the
-  // pair's samples, so rows g and g ^ 1 hold the same 16 samples (rows 0 / 1: 0-7, 16-23;
-  // rows 2 / 3: 8-15, 24-31), in an order whose row sums (DPP row_shr 8, 4, 2, 1) agree bit
-  // for bit
-  const int ls = 4 * ((g & 2) | ((g & 1) ^ (c >> 3))) + (c & 3) + 16 * ((c >> 2) & 1);
-  float* gw = J.w;
-  float wr[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int i = 16 * (j >> 2) + 4 * g + (j & 3);
-    wr[j] = i < nfsp::OBS ? gw[nn::OW1 + i * nn::H + hid] : i == CHAIN_BIAS_IN ? gw[nn::OB1 + hid] : 0.f;
-  }
-  float W2_0 = gw[nn::OW2 + 3 * hid + 0], W2_1 = gw[nn::OW2 + 3 * hid + 1], W2_2 = gw[nn::OW2 + 3 * hid + 2];
-  float b2_0 = gw[nn::OB2 + 0], b2_1 = gw[nn::OB2 + 1], b2_2 = gw[nn::OB2 + 2];
-  const int nmb = C.B / CHAIN_MB;
-  const int spu = C.E * nmb;                   // SGD steps per update
-  const float inv3m = 1.0f / (float)(3 * CHAIN_MB);
-  const float invm = 1.0f / (float)CHAIN_MB;
-  const int64_t u1 = J.u1;
-  int64_t u0 = J.u0;
-  if (J.active) {          // AR: skip the inactive prefix (M_SL <= batch; monotone in u)
-    while (u0 < u1) {
-      const int64_t q = u0 + l;
-      const unsigned long long m = __ballot(q < u1 && J.active[q]);
-      if (m) { u0 += __builtin_ctzll(m); break; }
-      u0 += 64;
-    }
-    if (u0 > u1) u0 = u1;
-  }
-  const int T1 = (int)(u1 * spu);
-  int t = (int)(u0 * spu);
-  // this wave's quarter of record p (clamped), into a register / back into ring slot p & 3;
-  // the lanes past the quarter load a duplicate chunk and store it to the sink.  The loads go
-  // through a buffer descriptor: the record offset is a scalar, the lane's chunk offset a
-  // loop-invariant VGPR (no 64-bit address arithmetic per step)
-  const bool in_q = l < REC_QUARTER;
-  const int la = in_q ? l : REC_QUARTER - 1;
-  const int T1c = T1 > 0 ? T1 : 1;
-  const auto rrsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<StepRec*>(J.rec), 0,
-                                                       (int)((size_t)T1c * sizeof(StepRec)), 0x00020000);
-  const int va_off = (REC_QUARTER * w + la) * 16;
-  auto issue = [&](int p, uint4& va) {
-    const int pc = p < T1 ? p : T1 - 1;
-    va = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rrsrc, va_off, pc * (int)sizeof(StepRec), 0));
-  };
-  // ring slot `slot` (a constant in the unrolled loop): lanes past the quarter store to the sink
-  auto stash_slot = [&](int slot, const uint4& va) {
-    uint4* dst = reinterpret_cast<uint4*>(&sm.ring[slot]) + REC_QUARTER * w;
-    *(in_q ? dst + l : &sm.rec_sink[l]) = va;
-  };
-  auto stash = [&](int p, const uint4& va) { stash_slot(p & 3, va); };
-  // X^T (the dW1 operand, K = samples) by transposed reads of the fa image: in each 16-lane
-  // group g, lane c = 4q + p supplies row q = sample 4g + q, columns 4p .. 4p + 3 = inputs
-  // 4p .. 4p + 3, i.e. the first 8 bytes of sample 4g + q's chunk of row p; lane c receives
-  // input c of samples 4g .. 4g + 3.  +256 B: samples 16 + 4g ..; +8 B: inputs 16 + 4p ..
-  // (ba1: input 16 + c).
-  const int tr_off = 512 * (c & 3) + 16 * fa_slot(c & 3, 4 * g + (c >> 2));
-  const int fsw = 12 * (g & 1);                // fa_slot(g, .) of this lane row
-  auto publish = [&]() {   // this wave's W2 rows for its own Z1^T layer 2
-    sm.w2t[w][l] = make_float4(W2_0, W2_1, W2_2, 0.f);
-  };
-  const SplitK SK = split_consts();
-  // W2 and b2 live in the wave's LDS (w2t rows 0..15, b2s); the cross-lane reductions leave
-  // each gradient total in one row of lanes (see the update), and that row owns the value:
-  //   row 0: W2[c][0]   row 1: W2[c][2]   row 2: W2[c][1]   row 3: b2[0]  (own1; row 3's total
-  //   is 4 gb2[0], scaled by 1/4 -- exact)        rows 0, 1: b2[1]   rows 2, 3: b2[2]  (own2)
-  float* const own1 = g == 3 ? &sm.b2s[w][0] : reinterpret_cast<float*>(&sm.w2t[w][c]) + (g == 0 ? 0 : g == 1 ? 2 : 1);
-  float* const own2 = &sm.b2s[w][g < 2 ? 1 : 2];
-  // NFSP_CHAIN_G0ROW (round 6): gb2[0] enters the V transpose as each row's own 16-sample sum
-  // (tot_rows) instead of the 32-sample total replicated in every lane (tot32: one permlane32 and
-  // a copy more); rows g and g ^ 1 hold the same 16 samples, so row 3's total is 2 gb2[0]
-  const float own1_sc = g == 3 ? (NFSP_CHAIN_G0ROW ? 0.5f : 0.25f) : 1.0f;
-#ifdef NFSP_CHAIN_STAMPS
-  unsigned long long st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_last = 0;
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_last)::"memory");
-  const unsigned long long st_t0 = st_last;
-#endif
-  // Records reach the lanes through an LDS ring: at step t each wave loads its quarter of
-  // record t + 2 and stores it at the end of step t; barrier(t + 1) publishes it.  Every
-  // load is consumed inside its own step (nothing loop-carried in registers), and the 4
-  // waves share one copy of each record.
-  float loss_acc = 0.f;                        // wave 0 lane 0: running epoch loss
-  // PH: t & 3 when the caller knows it at compile time (the loop unrolled by 4), else -1
-  auto step = [&](auto PHC) {
-    constexpr int PH = decltype(PHC)::value;
-    const int slot = PH >= 0 ? PH : (t & 3);
-    uint4 va;
-    issue(t + 2, va);
-    const StepRec& R = sm.ring[slot];
-    const bf16x8 fa0 = __builtin_bit_cast(bf16x8, R.fa[g][c ^ fsw]);
-    const bf16x8 fa1 = __builtin_bit_cast(bf16x8, R.fa[g][(16 + c) ^ fsw]);
-    // X^T, read where each chain measured fastest (tools/chain_ab.sh; results identical):
-    // BR right after the barrier, AR after the loss (round 3: after the dm reads).  Beside the fa reads both were
-    // slower (BR 0.831 -> 0.90 us, bimodal), as was carrying them from the previous step.
-    bf16x8 ba0, ba1;
-    const char* const rtr = reinterpret_cast<const char*>(&R.fa[0][0]) + tr_off;
-    // ---- layer 1, both orientations
-    bf16x8 whi, wmid, wlo;
-    split3(wr, whi, wmid, wlo, SK);
-    float W2h[4][3];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const floatx4 q = (PK & PK_L2) ? lds4v(&sm.w2t[w][4 * g + r]) : lds4(&sm.w2t[w][4 * g + r]);
-      W2h[r][0] = q[0]; W2h[r][1] = q[1]; W2h[r][2] = q[2];
-    }
-    const floatx4 w2c = lds4(&sm.w2t[w][c]);     // W2 of this lane's hidden unit (backward)
-    const float W2_0 = w2c[0], W2_1 = w2c[1], W2_2 = w2c[2];
-    const floatx4 b2v = lds4(&sm.b2s[w][0]);
-    const float b2_0 = b2v[0], b2_1 = b2v[1], b2_2 = b2v[2];
-    // Z1^T first (layer 2 waits on it); Z1 (needed only by the backward) is issued after
-    // layer 2, so its matrix-core time overlaps the barrier wait
-    const floatx4 zh0 = mfma3t(whi, wmid, wlo, fa0);     // Z1^T: hidden 16w+4g+r, sample c
-    const floatx4 zh1 = mfma3t(whi, wmid, wlo, fa1);     //                      sample 16+c
-    __builtin_amdgcn_sched_barrier(0);
-    CHAIN_STAMP(0);
-    // ---- layer 2 partial over the slice, from Z1^T
-    float p0[3], p1[3];
-    if constexpr (PK & PK_L2) {     // the two sample halves as pairs
-      floatx2 P[3];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) P[k] = floatx2{0.f, 0.f};
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const floatx2 H = {fmaxf(zh0[r], 0.f), fmaxf(zh1[r], 0.f)};
-#pragma unroll
-        for (int k = 0; k < 3; ++k)
-          P[k] = __builtin_elementwise_fma(H, floatx2{W2h[r][k], W2h[r][k]}, P[k]);
-      }
-#pragma unroll
-      for (int k = 0; k < 3; ++k) { p0[k] = P[k].x; p1[k] = P[k].y; }
-    } else {
-#pragma unroll
-      for (int k = 0; k < 3; ++k) { p0[k] = 0.f; p1[k] = 0.f; }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float h0 = fmaxf(zh0[r], 0.f);        // b1 is W1's row 30 (CHAIN_BIAS_IN)
-        const float h1 = fmaxf(zh1[r], 0.f);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          p0[k] = p0[k] + h0 * W2h[r][k];
-          p1[k] = p1[k] + h1 * W2h[r][k];
-        }
-      }
-    }
-    const int buf = PH >= 0 ? (PH & 1) : (t & 1);
-    float q[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {   // rows g, g ^ 2 (tile halves)
-      const auto rr = __builtin_amdgcn_permlane32_swap(__float_as_uint(p0[k]), __float_as_uint(p1[k]),
-                                                       false, false);
-      q[k] = __uint_as_float(rr[0]) + __uint_as_float(rr[1]);
-    }
-    {   // rows g, g ^ 1: outputs 0 and 1 in one swap (even rows get output 0's sum, odd rows
-        // output 1's), output 2 alone; every lane stores what it holds (same sums as before)
-      const auto r01 = __builtin_amdgcn_permlane16_swap(__float_as_uint(q[0]), __float_as_uint(q[1]), false, false);
-      float* const pr = &sm.po[buf][w][sl][0];
-      pr[g & 1] = __uint_as_float(r01[0]) + __uint_as_float(r01[1]);
-      pr[2] = sum_x16(q[2]);
-    }
-    // BR: the Z1 MFMAs and the targets' read fenced between the partial stores and the barrier
-    // (they overlap the barrier wait).  AR: left to the scheduler, which measured faster (AR
-    // 0.810 -> 0.787 us per SGD step; the BR chain unfenced 0.751 -> 0.786; tools/chain_ab.sh,
-    // results identical)
-    if (RELU) __builtin_amdgcn_sched_barrier(0);
-    const floatx4 zs0 = mfma3(fa0, whi, wmid, wlo);      // Z1: sample 4g+r, hidden 16w+c
-    const floatx4 zs1 = mfma3(fa1, whi, wmid, wlo);      //     sample 16+4g+r
-    const float4 tg = R.tg[ls];                          // read before the barrier pins it early
-    if (RELU) __builtin_amdgcn_sched_barrier(0);         // ... and the Z1 MFMAs issue before it
-    CHAIN_STAMP(1);
-    __syncthreads();
-    CHAIN_STAMP(2);
-    if (RELU) {
-      ba0 = tr_pair(rtr, rtr + 256);
-      ba1 = tr_pair(rtr + 8, rtr + 264);
-    }
-    // ---- output + loss of sample ls (every wave redundantly, identical results)
-    float d0, d1, d2, lr_step;
-    float o_keep[3], tt_keep[3], p_keep[3];     // for the optional loss log
-    {
-      constexpr bool vo = PK & PK_O;
-      const floatx4 a0 = vo ? lds4v(&sm.po[buf][0][ls][0]) : lds4(&sm.po[buf][0][ls][0]);
-      const floatx4 a1 = vo ? lds4v(&sm.po[buf][1][ls][0]) : lds4(&sm.po[buf][1][ls][0]);
-      const floatx4 a2 = vo ? lds4v(&sm.po[buf][2][ls][0]) : lds4(&sm.po[buf][2][ls][0]);
-      const floatx4 a3 = vo ? lds4v(&sm.po[buf][3][ls][0]) : lds4(&sm.po[buf][3][ls][0]);
-      float o0, o1;
-      if constexpr (PK & PK_O) {
-        const floatx2 o01 = (((a0.xy + a1.xy) + a2.xy) + a3.xy) + floatx2{b2_0, b2_1};
-        o0 = o01.x;
-        o1 = o01.y;
-      } else {
-        o0 = (((a0[0] + a1[0]) + a2[0]) + a3[0]) + b2_0;
-        o1 = (((a0[1] + a1[1]) + a2[1]) + a3[1]) + b2_1;
-      }
-      const float o2 = (((a0[2] + a1[2]) + a2[2]) + a3[2]) + b2_2;
-      lr_step = tg.w;
-      const float tt[3] = {tg.x, tg.y, tg.z};
-      o_keep[0] = o0; o_keep[1] = o1; o_keep[2] = o2;
-      tt_keep[0] = tg.x; tt_keep[1] = tg.y; tt_keep[2] = tg.z;
-      if (RELU) {          // Huber on ReLU outputs (RELU 2: linear outputs), mean over 3 x batch
-        const float oz[3] = {o0, o1, o2};
-        float dd[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          const float ee = tt[k] - (RELU >= 2 ? oz[k] : fmaxf(oz[k], 0.f));
-          // Huber: |e| > 1 ? sign(e) : e  ==  clamp(e, -1, 1); MSE (RELU 3): 2 e
-          const float gg = RELU == 3 ? ee * 2.0f : __builtin_amdgcn_fmed3f(ee, -1.f, 1.f);
-          dd[k] = (RELU >= 2 || oz[k] > 0.f) ? gg * -inv3m : 0.f;
-        }
-        d0 = dd[0]; d1 = dd[1]; d2 = dd[2];
-      } else {
-        // Keras categorical cross-entropy on the softmax (normalise p = y / S, clip p to
-        // [1e-7, 1 - 1e-7], loss -sum t log p; mean over the batch).  Its gradient w.r.t.
-        // the logits in closed form, with M = the unclipped outputs (the clip's gradient
-        // is 0 elsewhere) and T_M = sum_{k in M} t_k:
-        //   d_k = (y_k T_M / S - [k in M] t_k) / batch
-        // (the chain rule through normalise and softmax; the cancelling terms removed --
-        // oracle/nn_oracle.py evaluates the unsimplified chain)
-        // exp(o - mx) as exp2(o log2(e) - mx log2(e)): one fma per output instead of a subtract
-        // and a multiply.  The normalisation S = y0 + y1 + y2 is 1 within a few ulps (y is
-        // e / sum(e) by v_rcp_f32), so p = y / S is taken as y: two adds, a v_rcp_f32 and four
-        // multiplies off the loss's dependent chain (AR 7.08 -> 6.97 us per update; against the
-        // f32 reference chain, tools/bench_chain.hip compare, 2e-4 -> 7e-7 after 200 updates).
-        const float mx = fmaxf(fmaxf(o0, o1), o2);
-        const float L2E = 1.44269504088896341f, mxl = mx * L2E;
-        const float e0 = __builtin_amdgcn_exp2f(__builtin_fmaf(o0, L2E, -mxl));
-        const float e1 = __builtin_amdgcn_exp2f(__builtin_fmaf(o1, L2E, -mxl));
-        const float e2 = __builtin_amdgcn_exp2f(__builtin_fmaf(o2, L2E, -mxl));
-        const float rs = __builtin_amdgcn_rcpf((e0 + e1) + e2);
-        // outputs 0 / 1 as a pair (PK_SM): the same products, two per instruction
-        const floatx2 y01 = (PK & PK_SM) ? floatx2{e0, e1} * floatx2{rs, rs} : floatx2{e0 * rs, e1 * rs};
-        const float y0 = y01.x, y1 = y01.y, y2 = e2 * rs;
-        const float eps = 1e-7f, hi = 1.0f - 1e-7f;
-        const float q0 = y0, q1 = y1, q2 = y2;
-        p_keep[0] = q0; p_keep[1] = q1; p_keep[2] = q2;
-        // q in [eps, 1 - eps]  <=>  clamp(q, eps, 1 - eps) == q
-        const float m0 = __builtin_amdgcn_fmed3f(q0, eps, hi) == q0 ? tt[0] : 0.f;
-        const float m1 = __builtin_amdgcn_fmed3f(q1, eps, hi) == q1 ? tt[1] : 0.f;
-        const float m2 = __builtin_amdgcn_fmed3f(q2, eps, hi) == q2 ? tt[2] : 0.f;
-        // AR records carry t / batch (k_ar_prep; a power-of-two scale, exact), so the 1 / batch
-        // of both terms is already in m_k
-        const float k = (m0 + m1) + m2;
-        if constexpr (PK & PK_SM) {
-          const floatx2 d01 = __builtin_elementwise_fma(y01, floatx2{k, k}, -floatx2{m0, m1});
-          d0 = d01.x;
-          d1 = d01.y;
-        } else {
-          d0 = y0 * k - m0;
-          d1 = y1 * k - m1;
-        }
-        d2 = y2 * k - m2;
-      }
-    }
-    if (LOSS) {            // fit loss of this minibatch (before its update), Keras' epoch mean
-      float Ls;
-      if (RELU) {          // huber_loss with py2's 1 / 2 == 0: |e| > 1 ? |e| : e^2 / 2, mean over 3
-        float acc = 0.f;   // (RELU 3: e^2)
-        for (int k = 0; k < 3; ++k) {
-          const float e = tt_keep[k] - (RELU >= 2 ? o_keep[k] : fmaxf(o_keep[k], 0.f));
-          acc += RELU == 3 ? e * e : (fabsf(e) > 1.0f ? fabsf(e) : 0.5f * e * e);
-        }
-        Ls = acc * (1.0f / 3.0f);
-      } else {             // categorical cross-entropy: -sum t log(clip(y / S))
-        float acc = 0.f;
-        for (int k = 0; k < 3; ++k)      // (tt_keep = t / batch)
-          acc -= (tt_keep[k] * (float)CHAIN_MB) * __logf(fminf(fmaxf(p_keep[k], 1e-7f), 1.0f - 1e-7f));
-        Ls = acc;
-      }
-      const float x = tot32(Ls);             // the 32 samples, round-3 order
-      if (w == 0 && l == 0) {
-        const int in_u = t % spu;
-        loss_acc += x * invm;
-        if (in_u % nmb == nmb - 1) {
-          const int64_t uu = t / spu, ee = in_u / nmb;
-          J.loss_out[uu * C.E + ee] = loss_acc / (float)nmb;
-          loss_acc = 0.f;
-        }
-      }
-    }
-    // gb2 = the 32-sample sums of d (round-3 order): gb2[0] in every lane, gb2[1] in rows 0 / 1
-    // and gb2[2] in rows 2 / 3 (U, the rows that own b2[1] / b2[2])
-    const float G0 = NFSP_CHAIN_G0ROW ? tot_rows(d0) : tot32(d0);
-    const float U = tot32_pair(d1, d2);
-    CHAIN_STAMP(3);
-    // ---- backward in the sample-major layout: samples 16 mt + 4g + r, hidden 16w + c
-    if (!RELU) {
-      ba0 = tr_pair(rtr, rtr + 256);
-      ba1 = tr_pair(rtr + 8, rtr + 264);
-    }
-    float dz[8];
-    float g2_0, g2_1, g2_2;          // started by slot 0 (bwd_dpp<0>)
-    {
-      const float zz[8] = {zs0[0], zs0[1], zs0[2], zs0[3], zs1[0], zs1[1], zs1[2], zs1[3]};
-      float dh[8];
-#define NFSP_BWD_SLOT(J) dh[J] = bwd_dpp<J>(g2_0, g2_1, g2_2, d0, d1, d2, fmaxf(zz[J], 0.f), W2_0, W2_1, W2_2)
-      NFSP_BWD_SLOT(0); NFSP_BWD_SLOT(1); NFSP_BWD_SLOT(2); NFSP_BWD_SLOT(3);
-      NFSP_BWD_SLOT(4); NFSP_BWD_SLOT(5); NFSP_BWD_SLOT(6); NFSP_BWD_SLOT(7);
-#undef NFSP_BWD_SLOT
-#pragma unroll
-      for (int j = 0; j < 8; ++j) dz[j] = zz[j] > 0.f ? dh[j] : 0.f;
-    }
-    bf16x8 dhi, dmid, dlo;
-    split3(dz, dhi, dmid, dlo, SK);
-    // dW1[16 it + 4g + r][16w + c] = sum over the 32 samples in dz's K order (row 30: gb1)
-    const floatx4 gA = mfma3(ba0, dhi, dmid, dlo);
-    const floatx4 gB = mfma3(ba1, dhi, dmid, dlo);
-    // The four row totals of (g2_0, g2_1, g2_2, gb2[0]) in one transpose: two swaps across
-    // rows g ^ 2, one across g ^ 1 leave g2_0's total in row 0, g2_2's in row 1, g2_1's in row 2
-    // and 4 gb2[0] in row 3 (gb2[0] is in every row), each added (r0 + r2) + (r1 + r3) as
-    // sum_x16(sum_x32(.)) did.  Each row updates the values it holds (own1, own2).
-    float V;
-    {
-      const auto ab = __builtin_amdgcn_permlane32_swap(__float_as_uint(g2_0), __float_as_uint(g2_1), false, false);
-      const float tab = __uint_as_float(ab[0]) + __uint_as_float(ab[1]);
-      const auto cd = __builtin_amdgcn_permlane32_swap(__float_as_uint(g2_2), __float_as_uint(G0), false, false);
-      const float tcd = __uint_as_float(cd[0]) + __uint_as_float(cd[1]);
-      const auto z = __builtin_amdgcn_permlane16_swap(__float_as_uint(tab), __float_as_uint(tcd), false, false);
-      V = __uint_as_float(z[0]) + __uint_as_float(z[1]);
-    }
-    CHAIN_STAMP(4);
-    const float lr = lr_step;
-    {
-      const float v1 = *own1, v2 = *own2;
-      *own1 = v1 - (lr * own1_sc) * V;
-      *own2 = v2 - lr * U;
-    }
-    if constexpr (PK & PK_W) {      // W1 -= lr dW1, two rows per instruction
-      const floatx2 nl = {-lr, -lr};
-#pragma unroll
-      for (int r = 0; r < 4; r += 2) {
-        const floatx2 a = __builtin_elementwise_fma(nl, floatx2{gA[r], gA[r + 1]}, floatx2{wr[r], wr[r + 1]});
-        const floatx2 b = __builtin_elementwise_fma(nl, floatx2{gB[r], gB[r + 1]}, floatx2{wr[4 + r], wr[5 + r]});
-        wr[r] = a.x; wr[r + 1] = a.y; wr[4 + r] = b.x; wr[5 + r] = b.y;
-      }
-    } else {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        wr[r] = wr[r] - lr * gA[r];
-        wr[4 + r] = wr[4 + r] - lr * gB[r];
-      }
-    }
-    stash_slot(PH >= 0 ? ((PH + 2) & 3) : ((t + 2) & 3), va);
-    CHAIN_STAMP(5);
-  };
-  if (t < T1) {
-    {
-      uint4 va;
-      issue(t, va);
-      stash(t, va);
-      issue(t + 1, va);
-      stash(t + 1, va);
-    }
-    publish();
-    if (l < 3) sm.b2s[w][l] = l == 0 ? b2_0 : l == 1 ? b2_1 : b2_2;
-    __syncthreads();
-    // drain the prologue's loads: the loop header then merges no pending load into the
-    // registers the loop reuses (else every step waits on its fresh record load)
-    __builtin_amdgcn_s_waitcnt(0x0F70);            // vmcnt(0) (gfx9 encoding: expcnt 7, lgkmcnt 15)
-    if (spu % 4 == 0) {    // t and T1 are multiples of 4: ring slots and po buffers are constants
-      for (; t < T1; ++t) {
-        step(std::integral_constant<int, 0>{});
-        ++t;
-        step(std::integral_constant<int, 1>{});
-        ++t;
-        step(std::integral_constant<int, 2>{});
-        ++t;
-        step(std::integral_constant<int, 3>{});
-      }
-    } else {
-      for (; t < T1; ++t) step(std::integral_constant<int, -1>{});
-    }
-  }
-#ifdef NFSP_CHAIN_STAMPS
-  if (l == 0) {
-    unsigned long long t_end;
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_end)::"memory");
-    st_acc[8] = t_end - st_t0;
-    st_acc[9] = (unsigned long long)(T1 - (int)(u0 * spu));
-    if (C.stamps) {
-      for (int k = 0; k < 10; ++k) C.stamps[(blockIdx.x * 4 + w) * 10 + k] = st_acc[k];
-    } else {       // engine build: accumulate per (net, block, wave) for nfsp_debug_chain_stamps
-      if (!TABLE && blockIdx.x < 2)
-        for (int k = 0; k < 10; ++k) atomicAdd(&g_chain_stamps[RELU * 2 + blockIdx.x][w][k], st_acc[k]);
-    }
-  }
-#endif
-  if (t > (int)(u0 * spu)) {             // the loop ran: W2 / b2 as the last step left them
-    const float4 fw = sm.w2t[w][c];
-    W2_0 = fw.x; W2_1 = fw.y; W2_2 = fw.z;
-    b2_0 = sm.b2s[w][0]; b2_1 = sm.b2s[w][1]; b2_2 = sm.b2s[w][2];
-  }
-  float* dsts[3] = {gw, J.sync_to, J.snap_to};
-  for (int k = 0; k < 3; ++k) {
-    float* dst = dsts[k];
-    if (!dst) continue;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int i = 16 * (j >> 2) + 4 * g + (j & 3);
-      if (i < nfsp::OBS) dst[nn::OW1 + i * nn::H + hid] = wr[j];
-      else if (i == CHAIN_BIAS_IN) dst[nn::OB1 + hid] = wr[j];
-    }
-    if (g == 0) {
-      dst[nn::OW2 + 3 * hid + 0] = W2_0;
-      dst[nn::OW2 + 3 * hid + 1] = W2_1;
-      dst[nn::OW2 + 3 * hid + 2] = W2_2;
-    }
-    if (w == 0 && l == 0) {
-      dst[nn::OB2 + 0] = b2_0;
-      dst[nn::OB2 + 1] = b2_1;
-      dst[nn::OB2 + 2] = b2_2;
-    }
-  }
+#include "chain3_body.inc"
+}
+
+// One job's chain as a device function (k_br_persist, learner.hip): the same body
+template <int RELU, int LOSS, int TABLE>
+__device__ __forceinline__ void chain3_run(const ChainArgs& C, const ChainJob J, char* smem_raw) {
+  Chain3Smem& sm = *reinterpret_cast<Chain3Smem*>(smem_raw);
+#include "chain3_body.inc"
 }
 
 

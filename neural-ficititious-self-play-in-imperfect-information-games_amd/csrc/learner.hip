@@ -287,89 +287,163 @@ struct TargetJob {
 __global__ void __launch_bounds__(256) k_br_targets(const TargetJob* __restrict__ jobs, TargetJob one,
                                                     int B, int E, double gamma, unsigned quirks,
                                                     double lr0) {
-  // threads 0..127: Q_target(s) of row b (waves 0-1); threads 128..255: Q_target(s2) of
-  // row b - 128 (waves 2-3) -- the two forwards of a row run side by side
-  __shared__ __attribute__((aligned(16))) float sw[NET_LDS];
-  __shared__ float q[MAX_BATCH][3];
-  __shared__ float val[MAX_BATCH];
-  __shared__ uint32_t sb[MAX_BATCH];
-  __shared__ uint8_t am[MAX_BATCH];
-  __shared__ double part[2];
-  __shared__ int lastw[2][3];
   const TargetJob J = jobs ? jobs[blockIdx.y] : one;
-  if ((int64_t)blockIdx.x >= J.n) return;            // block-uniform
-  const int tid = threadIdx.x;
-  const int b = tid & (MAX_BATCH - 1);
-  const bool s2half = tid >= MAX_BATCH;
-  const int64_t u = J.u0 + blockIdx.x;
-  BrRow rr{};
-  if (b < B) rr = J.rows[u * B + b];
-  // the records of epoch e are emitted by threads 128 (e & 1) .. + 127 (below); their fit
-  // order is loaded now, beside the net
-  const int half = tid >> 7;
-  int pk[2] = {0, 0};
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int e = half + 2 * k;
-    if (e < E && b < B) pk[k] = J.perm[(u * E + e) * B + b];
-  }
-  stage_net_lds(sw, J.tw, tid, blockDim.x);
-  __syncthreads();
-  if (b < B) {
-    float y[3];
-    if (!s2half) {
-      fwd_lds(sw, rr.s, br_act(quirks), y);
-      q[b][0] = y[0]; q[b][1] = y[1]; q[b][2] = y[2];
-      am[b] = (uint8_t)(rr.meta & 0xFFu);
-      sb[b] = rr.s;
-    } else {
-      fwd_lds(sw, rr.s2, br_act(quirks), y);
-      const float qmax = fmaxf(fmaxf(y[0], y[1]), y[2]);
-      const float r = (float)(int8_t)((rr.meta >> 16) & 0xFFu) * 0.5f;
-      const bool terminal = !(quirks & NFSP_QUIRK_TERMINAL_BOOTSTRAP) && ((rr.meta >> 8) & 1u);
-      val[b] = (float)(terminal ? (double)r : (double)r + gamma * (double)qmax);
+  const int64_t bx = blockIdx.x;
+#include "br_targets_body.inc"
+}
+
+// one update's targets by the calling workgroup (k_br_persist's helpers): the same body
+__device__ __forceinline__ void br_targets_item(const TargetJob J, int64_t bx, int B, int E, double gamma,
+                                                unsigned quirks, double lr0) {
+#include "br_targets_body.inc"
+}
+
+// ---------------------------------------------------------------------------
+// k_br_persist: an engine group's whole BR learner call in one launch (nfsp_group_sched.br_persist;
+// round 5, re-landed in round 6 -- DESIGN.md Appendix A.1b).  Workgroups 0 .. njobs - 1 are
+// chains, one per (replica, agent) with BR work: each runs its target-sync segments in order,
+// in pieces of `chunk` updates, each piece as soon as its targets are written.  The others are
+// helpers: they take work items -- (segment, update) -- in queue order and write that update's
+// targets and step records (k_br_targets' body).  The host queues the first segments' items; a
+// chain queues its next segment's items once the segment's last piece has synced the target
+// net they read.  No round waits for another job's segment and no targets launch sits between
+// chains.  The same SGD steps as the rounds, bit for bit (a piece resumes from the weights in
+// memory).
+// Hand-offs, agent scope (per-XCD L2s): the writer's stores, __threadfence in every writing
+// thread, the workgroup barrier, then one release atomic; the reader polls relaxed in one
+// thread, then one acquire fence and the workgroup barrier.  Every wait is bounded (spin x
+// s_sleep 8): on expiry *err is set and the workgroup leaves, so a lost hand-off ends the
+// kernel; the host reports it (group_check_err).
+// Loop shape: each loop has ONE thread-0 region per iteration, at its top, and the iteration
+// ends on a barrier.  The round-5 form also had a thread-0 region at the bottom (the helper's
+// "item done" atomic); the compiler merged the two across the back edge into a loop of their
+// own, which left the barrier-bearing body as an inner loop that lanes 1-63 of wave 0 and waves
+// 1-3 iterated on the stale work word while lane 0 waited for them to leave it: the hang of
+// profiles/r05_group_br_persist (found in round 6 in the ISA, profiles/r06/persist_rootcause).
+// ---------------------------------------------------------------------------
+struct BrPersistArgs {
+  ChainArgs C;                  // B, E (the chains' jobs come from seg_job)
+  const ChainJob* seg_job;      // [nseg] chain job of each segment (u0, u1: the segment; sync_to)
+  const TargetJob* seg_tgt;     // [nseg] its targets job
+  const int32_t* seg_chunk0;    // [nseg] its first chunk counter
+  const int32_t* job_seg0;      // [njobs + 1] chain workgroup j's segments: [job_seg0[j], job_seg0[j + 1])
+  uint32_t* slots;              // [nitems] work items (segment << 16 | update in it); BRP_EMPTY until queued
+  uint32_t* ctr;                // [0] helpers' claims, [1] queue reservations
+  uint32_t* chunk_done;         // finished items per chunk
+  int32_t* err;                 // pinned host: [0] a wait expired, [1] chain bails, [2] helper bails
+  int njobs, nitems, chunk;
+  int spin;                     // bound of every wait (s_sleep 8 rounds)
+  double gamma, lr0;
+  unsigned quirks;
+};
+constexpr uint32_t BRP_EMPTY = 0xFFFFFFFFu, BRP_DONE = 0xFFFFFFFEu;
+constexpr int BRP_SPIN = 1 << 18;           // x s_sleep 8 (~56 ms): far past any legitimate wait
+constexpr int BRP_CHUNK = 16;               // updates per chain piece (readiness is checked per piece)
+constexpr int BRP_HELPERS = 48;             // helper workgroups (c4_emul_r8: 96 / 160 took the
+                                            // step 217.7 -> 207.2 / 205.2 ms; the rounds 179.6)
+constexpr int BRP_STATIC_LDS = 16 * 1024;   // bound on the kernel's static LDS (the targets buffers)
+
+__device__ __forceinline__ void brp_bail(int32_t* err, int k) {
+  __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_fetch_add(err + k, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void __launch_bounds__(256) k_br_persist(BrPersistArgs P) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  __shared__ uint32_t s_word;
+  if ((int)blockIdx.x < P.njobs) {                         // ---- a chain
+    const int j = blockIdx.x;
+    for (int s = P.job_seg0[j]; s < P.job_seg0[j + 1]; ++s) {
+      const ChainJob JS = P.seg_job[s];
+      for (int64_t a = JS.u0, c = 0; a < JS.u1; a += P.chunk, ++c) {
+        const int64_t b = a + P.chunk < JS.u1 ? a + P.chunk : JS.u1;
+        if (threadIdx.x == 0) {                            // the iteration's one thread-0 region
+          const uint32_t* done = &P.chunk_done[P.seg_chunk0[s] + c];
+          int it = 0;
+          while (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)(b - a) &&
+                 ++it < P.spin)
+            __builtin_amdgcn_s_sleep(8);
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          s_word = it >= P.spin;
+          if (s_word) brp_bail(P.err, 1);
+        }
+        __syncthreads();
+        if (s_word) return;                                // workgroup-uniform
+        ChainJob JP = JS;
+        JP.u0 = a;
+        JP.u1 = b;
+        if (b < JS.u1) JP.sync_to = nullptr;               // the segment's last piece syncs
+        chain3_run<1, 0, 1>(P.C, JP, smem_raw);
+        __threadfence();        // the piece's weights (and synced target net) out, for the next
+        __syncthreads();        // piece's loads by other waves and for the helpers
+      }
+      if (s + 1 < P.job_seg0[j + 1]) {                     // queue the next segment's items
+        const uint32_t m = (uint32_t)P.seg_tgt[s + 1].n;
+        if (threadIdx.x == 0) s_word = __hip_atomic_fetch_add(&P.ctr[1], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        const uint32_t base = s_word;
+        for (uint32_t i = threadIdx.x; i < m; i += blockDim.x)
+          __hip_atomic_store(&P.slots[base + i], ((uint32_t)(s + 1) << 16) | i, __ATOMIC_RELEASE,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();        // s_word is rewritten by the next wait
+      }
     }
+    return;
   }
-  __syncthreads();
-  const int lane = tid & 63, wv = tid >> 6;
-  if (!s2half) {
-    // exploitability proxy (agent/agent.py:235-238): mean of the row maxima, before the
-    // row-0 overwrite; and for the quirk, the last row k with argmax a_k == action
-    double m = b < B ? (double)fmaxf(fmaxf(q[b][0], q[b][1]), q[b][2]) : 0.0;
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) m += __shfl_xor(m, off);
-    if (lane == 0) part[wv] = m;
-#pragma unroll
-    for (int act = 0; act < 3; ++act) {
-      const unsigned long long bal = __ballot(b < B && am[b] == act);
-      if (lane == 0) lastw[wv][act] = bal ? 64 * wv + 63 - __builtin_clzll(bal) : -1;
+  uint32_t* prev_done = nullptr;                           // thread 0: the last item's chunk counter
+  for (;;) {                                                // ---- a helper
+    if (threadIdx.x == 0) {                                // the iteration's one thread-0 region:
+      if (prev_done)                                       // publish the last item, take the next
+        __hip_atomic_fetch_add(prev_done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t p = __hip_atomic_fetch_add(&P.ctr[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      uint32_t v = BRP_DONE;
+      if (p < (uint32_t)P.nitems) {
+        int it = 0;
+        while ((v = __hip_atomic_load(&P.slots[p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == BRP_EMPTY &&
+               ++it < P.spin)
+          __builtin_amdgcn_s_sleep(8);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (v == BRP_EMPTY) {
+          brp_bail(P.err, 2);
+          v = BRP_DONE;
+        }
+      }
+      s_word = v;
     }
+    __syncthreads();
+    const uint32_t v = s_word;
+    __syncthreads();
+    if (v == BRP_DONE) return;                             // workgroup-uniform
+    const int s = (int)(v >> 16);
+    const int64_t i = (int64_t)(v & 0xFFFFu);
+    br_targets_item(P.seg_tgt[s], i, P.C.B, P.C.E, P.gamma, P.quirks, P.lr0);
+    __threadfence();
+    __syncthreads();
+    prev_done = &P.chunk_done[P.seg_chunk0[s] + i / P.chunk];
   }
-  __syncthreads();
-  if (tid == 0) J.expl[u] = (part[0] + part[1]) / B;
-  if (quirks & NFSP_QUIRK_ROW0_TARGET) {
-    if (tid < 3) {       // target[0][argmax a_k] = v_k for k = 0..B-1: the last k wins
-      const int last = lastw[1][tid] >= 0 ? lastw[1][tid] : lastw[0][tid];
-      if (last >= 0) q[0][tid] = val[last];
-    }
-  } else if (!s2half && b < B) {
-    q[b][am[b]] = val[b];
+}
+
+// launch with a CU per workgroup: dynamic LDS up to what the CU has left beside the kernel's
+// static LDS (the helpers' targets buffers), as the one-engine chains reserve theirs
+int launch_br_persist(const BrPersistArgs& P, int helpers, hipStream_t s) {
+  static std::atomic<uint64_t> mask{0};
+  static std::atomic<int> dyn{0};
+  int dev = 0;
+  NFSP_HIP(hipGetDevice(&dev));
+  const uint64_t bit = 1ull << (dev & 63);
+  if (!(mask.load(std::memory_order_acquire) & bit)) {
+    hipFuncAttributes fa{};
+    NFSP_HIP(hipFuncGetAttributes(&fa, (const void*)k_br_persist));
+    if ((int)fa.sharedSizeBytes > BRP_STATIC_LDS) return nfsp::fail(NFSP_EINVAL, "k_br_persist: static LDS");
+    const int d = CHAIN_LDS - BRP_STATIC_LDS;
+    if (d < (int)sizeof(Chain3Smem)) return nfsp::fail(NFSP_EINVAL, "k_br_persist: LDS");
+    NFSP_HIP(hipFuncSetAttribute((const void*)k_br_persist, hipFuncAttributeMaxDynamicSharedMemorySize, d));
+    dyn.store(d, std::memory_order_release);
+    mask.fetch_or(bit, std::memory_order_acq_rel);
   }
-  __syncthreads();
-  // lr of this update: lr0 / (1 + 0.003 sqrt(iteration)) with iteration = it0 + 2 u
-  // (agent/agent.py:249, iteration += 2 per BR update), in the reference's double arithmetic
-  const float lr = (float)(lr0 / (1.0 + 0.003 * sqrt((double)(J.it0 + 2 * u))));
-  // epochs in pairs: threads 0..127 emit epoch e, threads 128..255 epoch e + 1
-  for (int e = half, k = 0; e < E; e += 2, ++k) {
-    uint32_t x = 0;
-    float t0 = 0.f, t1 = 0.f, t2 = 0.f;
-    if (b < B) {
-      const int r = k < 2 ? pk[k] : J.perm[(u * E + e) * B + b];
-      x = sb[r];
-      t0 = q[r][0]; t1 = q[r][1]; t2 = q[r][2];
-    }
-    emit_recs(J.rec + (u * E + e) * (B / CHAIN_MB), x, t0, t1, t2, lr, B, b);
-  }
+  k_br_persist<<<P.njobs + helpers, 256, dyn.load(std::memory_order_acquire), s>>>(P);
+  NFSP_LAUNCHED("k_br_persist");
+  return NFSP_OK;
 }
 
 // schedule state after the learner (host-computed values + device-side counters)
@@ -925,6 +999,7 @@ struct nfsp_group {
   int64_t calls = 0;             // learner calls (slices) so far
   int64_t rounds = 0;            // BR rounds of the last learner call (stats)
   nfsp_group_sched sched{};      // nfsp_group_set_sched (from nfsp_group_default_sched)
+  int32_t* h_err = nullptr;      // k_br_persist's bail flags (pinned host, mapped): group_check_err
   int chain_lds = 0;             // LDS per chain workgroup: 4R chains on the device's CUs
   bool trace_on = false;         // nfsp_group_set_trace: per call [R][2][AR, BR] update counts
   std::vector<int32_t> trace;
@@ -956,6 +1031,7 @@ extern "C" int nfsp_group_destroy(nfsp_group* g) {
       if (ev) (void)hipEventDestroy(ev);
   }
   if (g->h_st) (void)hipHostFree(g->h_st);
+  if (g->h_err) (void)hipHostFree(g->h_err);
   for (void* p : {(void*)g->d_war, (void*)g->w0, g->d_roll, (void*)g->d_stp, (void*)g->d_st})
     if (p) (void)hipFree(p);
   for (hipStream_t st : {g->s_ar, g->s_br})
@@ -1033,6 +1109,8 @@ extern "C" int nfsp_group_create(nfsp_ctx* ctx, const nfsp_engine_cfg* cfg, int 
   if (r == hipSuccess) r = hipMalloc((void**)&g->d_stp, sizeof(EngineDev*) * replicas);
   if (r == hipSuccess) r = hipMalloc((void**)&g->d_st, sizeof(EngineDev) * replicas);
   if (r == hipSuccess) r = hipHostMalloc((void**)&g->h_st, sizeof(EngineDev) * replicas, hipHostMallocDefault);
+  if (r == hipSuccess) r = hipHostMalloc((void**)&g->h_err, sizeof(int32_t) * 4, hipHostMallocMapped | hipHostMallocCoherent);
+  if (r == hipSuccess) memset(g->h_err, 0, sizeof(int32_t) * 4);
   if (r == hipSuccess) r = hipMemcpy(g->d_stp, stp.data(), sizeof(EngineDev*) * replicas, hipMemcpyHostToDevice);
   if (r != hipSuccess) {
     nfsp_group_destroy(g);
@@ -1099,6 +1177,19 @@ struct TabCursor {
 // results on the BR stream after the last round; the exchange (when due) follows the AR chains
 // on the AR stream; with snap_after each learner stream then copies its nets into snapshot
 // `par` and records snap_ev[par] for the rollout two slices on.
+// k_br_persist's bounded waits: a hand-off that never came ended that kernel with a bail flag
+// set (pinned host memory).  Checked once the kernel has completed: after a learner call's
+// readback sync (the ctx stream has then waited for every earlier slice's BR stream) and by
+// nfsp_group_check (which synchronises first).
+static int group_check_err(nfsp_group* g) {
+  volatile int32_t* h = g->h_err;
+  if (!h || !h[0]) return NFSP_OK;
+  const int cb = h[1], hb = h[2];
+  h[0] = h[1] = h[2] = 0;
+  return nfsp::fail(NFSP_EHIP, "k_br_persist: a bounded wait expired (work-queue hand-off): chain bails " +
+                                   std::to_string(cb) + ", helper bails " + std::to_string(hb));
+}
+
 static int group_update(nfsp_group* g, bool pipelined = false, int par = 0, bool snap_after = false) {
   hipStream_t s = g->ctx->stream;
   const int R = g->R;
@@ -1110,9 +1201,10 @@ static int group_update(nfsp_group* g, bool pipelined = false, int par = 0, bool
   NFSP_LAUNCHED("k_gather_st");
   NFSP_HIP(hipMemcpyAsync(g->h_st, g->d_st, sizeof(EngineDev) * R, hipMemcpyDeviceToHost, s));
   NFSP_HIP(hipStreamSynchronize(s));
+  int rc;
+  if ((rc = group_check_err(g)) != NFSP_OK) return rc;
   KTimer kt(e0, KT_LEARNER);
   std::vector<LearnPlan> L(R);
-  int rc;
   int64_t maxU = 0, maxUbr = 0, maxSL = 0;
   const bool loss_log = e0->log_loss;
   for (int r = 0; r < R; ++r) {
@@ -1160,10 +1252,15 @@ static int group_update(nfsp_group* g, bool pipelined = false, int par = 0, bool
   // are short: the targets between them were ~10% of c4_emul_r8's BR stream); groups whose
   // chains share CUs keep one stream.
   const bool shared_cus = g->chain_lds < CHAIN_LDS;
+  // The persistent BR kernel (sched.br_persist) instead of the rounds: one launch, one stream,
+  // the reference's BR net (k_chain3<1>), no loss log, its 2R chains and BRP_HELPERS helpers a
+  // CU each beside the 2R AR chains (R <= 32, no CU sharing)
+  const bool persist = g->sched.br_persist && !loss_log && !(cfg.quirks & NFSP_EXT_LINEAR_Q) && R <= 32 &&
+                       !shared_cus;
   int nbs = g->sched.br_streams > 0 ? g->sched.br_streams : (e0->slices > 1 ? 2 : 1);
   nbs = nbs > GROUP_BR_STREAMS ? GROUP_BR_STREAMS : nbs;
   nbs = nbs > R ? R : nbs;
-  if (shared_cus) nbs = 1;
+  if (shared_cus || persist) nbs = 1;
   struct BrCursor {
     int r, a;
     size_t s;        // current segment
@@ -1180,7 +1277,7 @@ static int group_update(nfsp_group* g, bool pipelined = false, int par = 0, bool
   int pr0[GROUP_BR_STREAMS + 1];
   for (int p = 0; p <= nbs; ++p) pr0[p] = p * R / nbs;
   int64_t max_rounds = 0;
-  for (int p = 0; p < nbs; ++p) {
+  for (int p = 0; p < (persist ? 0 : nbs); ++p) {
     std::vector<BrCursor> bc;
     for (int r = pr0[p]; r < pr0[p + 1]; ++r)
       for (int a = 0; a < 2; ++a)
@@ -1229,11 +1326,51 @@ static int group_update(nfsp_group* g, bool pipelined = false, int par = 0, bool
     }
     max_rounds = nr > max_rounds ? nr : max_rounds;
   }
+  // k_br_persist's tables: each segment's chain and targets jobs, its chunk counters, and the
+  // work queue holding the first segments' items, chunk by chunk across the jobs
+  std::vector<ChainJob> p_job;
+  std::vector<TargetJob> p_tgt;
+  std::vector<int32_t> p_chunk0, p_jseg0;
+  std::vector<uint32_t> p_slots;
+  int32_t p_nchunks = 0;
+  uint32_t p_npre = 0;
+  if (persist) {
+    for (int r = 0; r < R; ++r)
+      for (int a = 0; a < 2; ++a) {
+        if (L[r].seg[a].empty()) continue;
+        p_jseg0.push_back((int32_t)p_job.size());
+        for (const Segment& sg : L[r].seg[a]) {
+          NFSP_REQUIRE(sg.v - sg.u < 65536, "a BR segment of >= 65536 updates");
+          p_job.push_back(br_chain_job(g->eng[r], a, sg));
+          p_tgt.push_back(br_target_job(g->eng[r], L[r], a, sg));
+          p_chunk0.push_back(p_nchunks);
+          p_nchunks += (int32_t)((sg.v - sg.u + BRP_CHUNK - 1) / BRP_CHUNK);
+        }
+      }
+    NFSP_REQUIRE(p_job.size() < 65536, "too many BR segments in one learner call");
+    const int njobs = (int)p_jseg0.size();
+    p_jseg0.push_back((int32_t)p_job.size());
+    int64_t nitems = 0, maxn = 0;
+    for (const TargetJob& t : p_tgt) nitems += t.n;
+    for (int j = 0; j < njobs; ++j) maxn = p_tgt[p_jseg0[j]].n > maxn ? p_tgt[p_jseg0[j]].n : maxn;
+    p_slots.assign((size_t)nitems, BRP_EMPTY);
+    for (int64_t c0 = 0; c0 < maxn; c0 += BRP_CHUNK)
+      for (int j = 0; j < njobs; ++j) {
+        const int sgi = p_jseg0[j];
+        const int64_t n = p_tgt[sgi].n, c1 = c0 + BRP_CHUNK < n ? c0 + BRP_CHUNK : n;
+        for (int64_t i = c0; i < c1; ++i) p_slots[p_npre++] = ((uint32_t)sgi << 16) | (uint32_t)i;
+      }
+    max_rounds = njobs > 0 ? 1 : 0;
+  }
   g->rounds = max_rounds;
   TabCursor cur;
   const size_t o_prep = cur.take<PrepArgs>(R), o_fin = cur.take<FinalArgs>(R);
   const size_t o_ar = cur.take<ChainJob>(ar_jobs.size()), o_br = cur.take<ChainJob>(br_jobs.size());
   const size_t o_tg = cur.take<TargetJob>(tg_jobs.size());
+  const size_t o_pj = cur.take<ChainJob>(p_job.size()), o_pt = cur.take<TargetJob>(p_tgt.size());
+  const size_t o_pc = cur.take<int32_t>(p_chunk0.size()), o_ps = cur.take<int32_t>(p_jseg0.size());
+  const size_t o_pq = cur.take<uint32_t>(p_slots.size()), o_pn = cur.take<uint32_t>(2);
+  const size_t o_pd = cur.take<uint32_t>((size_t)p_nchunks);
   const size_t need = cur.off;
   // Every earlier use of set `par` has completed: serially, the call starts with the readback's
   // sync; pipelined, the ctx stream waited for slice j - 2's snapshot events (after its chains)
@@ -1259,6 +1396,16 @@ static int group_update(nfsp_group* g, bool pipelined = false, int par = 0, bool
   memcpy(h_tab + o_ar, ar_jobs.data(), sizeof(ChainJob) * ar_jobs.size());
   memcpy(h_tab + o_br, br_jobs.data(), sizeof(ChainJob) * br_jobs.size());
   memcpy(h_tab + o_tg, tg_jobs.data(), sizeof(TargetJob) * tg_jobs.size());
+  if (persist) {
+    memcpy(h_tab + o_pj, p_job.data(), sizeof(ChainJob) * p_job.size());
+    memcpy(h_tab + o_pt, p_tgt.data(), sizeof(TargetJob) * p_tgt.size());
+    memcpy(h_tab + o_pc, p_chunk0.data(), sizeof(int32_t) * p_chunk0.size());
+    memcpy(h_tab + o_ps, p_jseg0.data(), sizeof(int32_t) * p_jseg0.size());
+    memcpy(h_tab + o_pq, p_slots.data(), sizeof(uint32_t) * p_slots.size());
+    const uint32_t ctr[2] = {0u, p_npre};
+    memcpy(h_tab + o_pn, ctr, sizeof(ctr));
+    memset(h_tab + o_pd, 0, sizeof(uint32_t) * (size_t)p_nchunks);
+  }
   const PrepArgs* d_prep = reinterpret_cast<const PrepArgs*>(d_tab + o_prep);
   const FinalArgs* d_fin = reinterpret_cast<const FinalArgs*>(d_tab + o_fin);
   const ChainJob* d_ar = reinterpret_cast<const ChainJob*>(d_tab + o_ar);
@@ -1327,6 +1474,28 @@ static int group_update(nfsp_group* g, bool pipelined = false, int par = 0, bool
   hipStream_t sp[GROUP_BR_STREAMS] = {g->s_br, g->s_brp[0], g->s_brp[1], g->s_brp[2]};
   for (int p = 0; p < nbs; ++p) NFSP_HIP(hipStreamWaitEvent(sp[p], fork_br, 0));
   KTimer kspan(e0, KT_BR_STREAM0, g->s_br);     // the group's BR streams, end to end (joined on s_br)
+  if (persist && p_jseg0.size() > 1) {
+    BrPersistArgs P{};
+    P.C.B = cfg.batch;
+    P.C.E = cfg.epochs;
+    P.seg_job = reinterpret_cast<const ChainJob*>(d_tab + o_pj);
+    P.seg_tgt = reinterpret_cast<const TargetJob*>(d_tab + o_pt);
+    P.seg_chunk0 = reinterpret_cast<const int32_t*>(d_tab + o_pc);
+    P.job_seg0 = reinterpret_cast<const int32_t*>(d_tab + o_ps);
+    P.slots = reinterpret_cast<uint32_t*>(d_tab + o_pq);
+    P.ctr = reinterpret_cast<uint32_t*>(d_tab + o_pn);
+    P.chunk_done = reinterpret_cast<uint32_t*>(d_tab + o_pd);
+    NFSP_HIP(hipHostGetDevicePointer((void**)&P.err, g->h_err, 0));
+    P.njobs = (int)p_jseg0.size() - 1;
+    P.nitems = (int)p_slots.size();
+    P.chunk = BRP_CHUNK;
+    P.spin = g->sched.br_persist > 1 ? g->sched.br_persist : BRP_SPIN;
+    P.gamma = cfg.gamma;
+    P.lr0 = cfg.lr_br;
+    P.quirks = cfg.quirks;
+    KTimer kc(e0, KT_CHAIN_BR, g->s_br);
+    if ((rc = launch_br_persist(P, BRP_HELPERS, g->s_br)) != NFSP_OK) return rc;
+  }
   for (const BrRound& rd : rounds_v) {
     hipStream_t st = sp[rd.p];
     const int nj = (int)(rd.b1 - rd.b0);
@@ -1501,6 +1670,7 @@ extern "C" int nfsp_group_default_sched(nfsp_group_sched* out) {
   out->br_pace = env_int("NFSP_GROUP_BR_PACE", 1) != 0;
   out->br_streams = env_int("NFSP_GROUP_BR_STREAMS", -1);
   out->serial = env_int("NFSP_GROUP_SERIAL", 0) != 0;
+  out->br_persist = env_int("NFSP_GROUP_BR_PERSIST", 0);
   return NFSP_OK;
 }
 
@@ -1509,6 +1679,7 @@ extern "C" int nfsp_group_set_sched(nfsp_group* g, const nfsp_group_sched* sc) {
   NFSP_REQUIRE(sc->br_cap >= -1, "br_cap must be >= -1");
   NFSP_REQUIRE(sc->br_streams == -1 || (sc->br_streams >= 1 && sc->br_streams <= GROUP_BR_STREAMS),
                "br_streams must be -1 or in [1, 4]");
+  NFSP_REQUIRE(sc->br_persist >= 0, "br_persist must be >= 0");
   g->sched = *sc;
   g->sched.br_pace = sc->br_pace != 0;
   g->sched.serial = sc->serial != 0;
@@ -1519,6 +1690,16 @@ extern "C" int nfsp_group_get_sched(nfsp_group* g, nfsp_group_sched* out) {
   NFSP_REQUIRE(g && out, "null argument");
   *out = g->sched;
   return NFSP_OK;
+}
+
+extern "C" int nfsp_group_check(nfsp_group* g) {
+  NFSP_REQUIRE(g, "null argument");
+  NFSP_HIP(hipStreamSynchronize(g->ctx->stream));
+  for (hipStream_t st : {g->s_ar, g->s_br})
+    if (st) NFSP_HIP(hipStreamSynchronize(st));
+  for (hipStream_t st : g->s_brp)
+    if (st) NFSP_HIP(hipStreamSynchronize(st));
+  return group_check_err(g);
 }
 
 extern "C" int nfsp_group_rounds(nfsp_group* g, int64_t* out) {

@@ -309,8 +309,8 @@ class EngineGroup:
         return {k: int(getattr(sc, k)) for k, _ in sc._fields_}
 
     def set_sched(self, **kw):
-        """nfsp_group_set_sched: change br_cap / br_pace / br_streams / serial from the next
-        learner call (the rest stay as they are).  No SGD step changes."""
+        """nfsp_group_set_sched: change br_cap / br_pace / br_streams / serial / br_persist
+        from the next learner call (the rest stay as they are).  No SGD step changes."""
         cur = self.sched()
         for k in kw:
             if k not in cur:
@@ -318,6 +318,11 @@ class EngineGroup:
         cur.update(kw)
         native.check(self.L.nfsp_group_set_sched(self.h, C.byref(native.GroupSched(**cur))),
                      "nfsp_group_set_sched")
+
+    def check(self):
+        """nfsp_group_check: synchronise the group's streams; raises if a k_br_persist wait
+        expired (sched br_persist)."""
+        native.check(self.L.nfsp_group_check(self.h), "nfsp_group_check")
 
     def rounds(self) -> int:
         n = native.I64()

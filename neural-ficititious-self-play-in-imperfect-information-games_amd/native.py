@@ -47,7 +47,7 @@ class EngineCfg(C.Structure):
 class GroupSched(C.Structure):
     """``nfsp_group_sched``: how a group schedules its BR rounds and slices (no result changes)"""
     _fields_ = [("br_cap", C.c_int32), ("br_pace", C.c_int32), ("br_streams", C.c_int32),
-                ("serial", C.c_int32)]
+                ("serial", C.c_int32), ("br_persist", C.c_int32)]
 
 
 class EngineStats(C.Structure):
@@ -127,6 +127,7 @@ SIGNATURES = {
     "nfsp_group_set_timing": (I32, [P, I32]),
     "nfsp_group_get_timings": (I32, [P, C.POINTER(F64), C.POINTER(I64)]),
     "nfsp_group_rounds": (I32, [P, C.POINTER(I64)]),
+    "nfsp_group_check": (I32, [P]),
     "nfsp_group_set_trace": (I32, [P, I32]),
     "nfsp_group_trace": (I32, [P, C.POINTER(I32), I64, C.POINTER(I64)]),
     "nfsp_group_set_exchange": (I32, [P, U32, I32, F32]),

@@ -223,12 +223,12 @@ def test_group_sched_changes_no_sgd_step(pkg):
     (a piece resumes from the weights in memory; the partitions run the same pieces)."""
     kw = dict(n_lanes=65_536, slices=16, slice_lag=2, rl_capacity=200_000, sl_capacity=400_000)
     variants = [None, dict(br_cap=0, br_pace=0, br_streams=1), dict(br_cap=16, br_pace=0, br_streams=4),
-                dict(br_cap=40, br_pace=1, br_streams=3), dict(serial=1)]
+                dict(br_cap=40, br_pace=1, br_streams=3), dict(serial=1), dict(br_persist=1)]
     runs = []
     for v in variants:
         g = pkg.engine.EngineGroup(4, seed=5151, init_seed=4, **kw)
         d = g.sched()
-        assert d == dict(br_cap=-1, br_pace=1, br_streams=-1, serial=0), d
+        assert d == dict(br_cap=-1, br_pace=1, br_streams=-1, serial=0, br_persist=0), d
         if v:
             g.set_sched(**v)
             assert all(g.sched()[k] == x for k, x in v.items())
@@ -236,6 +236,7 @@ def test_group_sched_changes_no_sgd_step(pkg):
         g.average_ar()
         for _ in range(2):
             g.step()
+        g.check()
         st = [r.stats() for r in g.replicas]
         assert min(min(s["br_updates"]) for s in st) > 300
         runs.append(([x.copy() for r in g.replicas for x in nets(r)], st, g.rounds()))
@@ -253,3 +254,67 @@ def test_group_sched_changes_no_sgd_step(pkg):
             g2.set_sched(br_streams=9)
         finally:
             g2.close()
+
+
+@pytest.mark.parametrize("R", [1, 3])
+def test_persistent_br_kernel_matches_standalone_engines(pkg, R):
+    """sched br_persist: a learner call's BR work as ONE k_br_persist launch (chain workgroups
+    taking 16-update pieces as 48 helper workgroups write the targets from a device work queue;
+    DESIGN.md Appendix A.1b).  Short target-sync segments (7 updates) make many hand-offs per
+    call.  Replicas stay bit-identical to standalone engines (which run the rounds' kernels)."""
+    g = pkg.engine.EngineGroup(R, seed=2024, init_seed=7, **SMALL)
+    g.set_sched(br_persist=1)
+    solo = [pkg.engine.SelfPlayEngine(seed=2024 + r, init_seed=7 + r, **SMALL) for r in range(R)]
+    for step in range(3):
+        g.step()
+        for e in solo:
+            e.step()
+        g.check()
+        assert g.rounds() == 1                     # one launch per learner call
+        for r in range(R):
+            a_st, b_st = g.replicas[r].stats(), solo[r].stats()
+            for k in STAT_KEYS:
+                assert a_st[k] == b_st[k], (step, r, k, a_st[k], b_st[k])
+            for x, y in zip(nets(g.replicas[r]), nets(solo[r])):
+                assert np.array_equal(x, y), (step, r)
+    assert min(g.replicas[0].stats()["target_syncs"]) >= 3
+    g.close()
+
+
+def test_persistent_br_kernel_c4_shape_matches_rounds(pkg):
+    """C4's group shape (8 replicas, pipelined slices, the AR exchange after every slice) with
+    the persistent BR kernel against the rounds: the same nets and counters bit for bit."""
+    kw = dict(n_lanes=131_072, slices=32, slice_lag=2, rl_capacity=200_000, sl_capacity=400_000)
+    runs = []
+    for persist in (0, 1):
+        g = pkg.engine.EngineGroup(8, seed=8080, init_seed=8, **kw)
+        g.set_sched(br_persist=persist)
+        g.set_exchange(pkg.native.XCHG_AR, every=1, scale=2.0 / 8)
+        g.average_ar()
+        for _ in range(2):
+            g.step()
+        g.check()
+        st = [r.stats() for r in g.replicas]
+        assert min(min(s["br_updates"]) for s in st) > 100
+        runs.append(([x.copy() for r in g.replicas for x in nets(r)], st))
+        g.close()
+    assert runs[0][1] == runs[1][1]
+    for x, y in zip(runs[0][0], runs[1][0]):
+        assert np.array_equal(x, y)
+
+
+def test_persistent_br_kernel_expired_wait_is_reported(pkg):
+    """br_persist > 1 bounds every device wait at that many s_sleep rounds.  At 2 the chains'
+    first waits expire before the helpers have written their targets: the kernel ends (it does
+    not hang) and nfsp_group_check reports the expired hand-off."""
+    g = pkg.engine.EngineGroup(2, seed=3, init_seed=1, **SMALL)
+    g.set_sched(br_persist=2)
+    g.step()
+    try:
+        g.check()
+    except pkg.native.NativeError as ex:
+        assert "bounded wait expired" in str(ex)
+    else:
+        pytest.skip("every hand-off was ready at its first poll (no wait expired)")
+    finally:
+        g.close()

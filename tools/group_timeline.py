@@ -28,6 +28,8 @@ def main():
     g = pkg.engine.EngineGroup(R, n_lanes=cfg["n_lanes"] // R, rl_capacity=cfg["rl_capacity"],
                                sl_capacity=cfg["sl_capacity"], seed=1234, init_seed=0,
                                avg_ar=not cfg.get("xchg_every"), **extra)
+    if cfg.get("sched"):
+        g.set_sched(**cfg["sched"])
     if cfg.get("xchg_every"):
         g.set_exchange(pkg.native.XCHG_AR, every=cfg["xchg_every"], scale=cfg["xchg_gain"] / R)
         g.average_ar()

@@ -48,6 +48,12 @@ PK_WINDOW = 32        # empirical: packed-f32 writes of any MFMA register
 PACKED = ("v_pk_fma_f32", "v_pk_mul_f32", "v_pk_add_f32")
 SOURCES = {"br": "learner.hip", "ar": "chain_ar.hip", "brlin": "chain_brlin.hip"}
 KERNEL_PREFIX = "_ZN4nfsp5chain8k_chain3"
+
+
+def is_chain_kernel(name: str) -> bool:
+    """A k_chain3 instance, or the persistent group BR kernel that runs the chain body inlined
+    (learner.hip k_br_persist)."""
+    return name.startswith(KERNEL_PREFIX) or "k_br_persist" in name
 _REG = re.compile(r"\b([vas])(?:(\d+)|\[(\d+):(\d+)\])")
 
 
@@ -106,7 +112,7 @@ def functions(asm_lines: list) -> dict:
     i = 0
     while i < len(asm_lines):
         l = asm_lines[i]
-        if l.startswith(KERNEL_PREFIX) and l.split(":")[0].endswith("E"):
+        if is_chain_kernel(l.split(":")[0]) and l.split(":")[0].endswith("E") and not l.startswith("."):
             name = l.split(":")[0]
             ins, labels, loops = [], {}, []
             j = i + 1
@@ -138,7 +144,7 @@ def functions_disassembled(text: str) -> dict:
     for line in text.split("\n") + [""]:
         m = re.match(r"^([0-9a-f]+) <(\S+)>:", line)
         if m or not line.strip():
-            if name and name.startswith(KERNEL_PREFIX) and ins:
+            if name and is_chain_kernel(name) and ins:
                 out[name] = (ins, loops)
             if m:
                 name, ins, addr_ix, loops = m.group(2), [], {}, []
