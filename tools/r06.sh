@@ -93,5 +93,11 @@ case "$1" in
       "60 for r in 1 0; do $A 200 \$r compare; $B 200 \$r compare; done > $O/chain_ab_$2_$3_compare.log" \
       "200 for i in 1 2 3; do for r in 1 0; do $A 2000 \$r time; $B 2000 \$r time; done; done > $O/chain_ab_$2_$3_time.log"
     ;;
+  brp)          # k_br_persist re-landed (profiles/r06/persist_rootcause): the group suite, then
+                # c4_emul_r8 with the rounds and with the persistent kernel in one bench process
+    ./tools/gpu_steps.sh \
+      "900 $PYT tests/test_gpu_group.py > $O/brp_group_tests.log" \
+      "900 python3 -u bench.py --no-cpu --groups c4_emul_r8,c4_emul_r8_persist --steps 5 --warmup 2 > $O/brp_bench_groups.json"
+    ;;
   *) echo "unknown job $1"; exit 2 ;;
 esac
