@@ -343,6 +343,13 @@ constexpr int BRP_HELPERS = 48;             // helper workgroups (c4_emul_r8: 96
                                             // step 217.7 -> 207.2 / 205.2 ms; the rounds 179.6)
 constexpr int BRP_STATIC_LDS = 16 * 1024;   // bound on the kernel's static LDS (the targets buffers)
 
+#ifdef NFSP_BRP_STAMPS
+// diagnostic build only (tools/build_lib_variant.py brpst -DNFSP_BRP_STAMPS=1, tools/brp_stamps.py):
+// per chain [wait cycles, chain cycles, SGD steps, pieces], per helper [wait, work, items, 0]
+__device__ unsigned long long g_brp_stamps[2][64][4];
+#define BRP_T() __builtin_amdgcn_s_memtime()
+#endif
+
 __device__ __forceinline__ void brp_bail(int32_t* err, int k) {
   __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_fetch_add(err + k, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -351,6 +358,9 @@ __device__ __forceinline__ void brp_bail(int32_t* err, int k) {
 __global__ void __launch_bounds__(256) k_br_persist(BrPersistArgs P) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   __shared__ uint32_t s_word;
+#ifdef NFSP_BRP_STAMPS
+  unsigned long long st_wait = 0, st_chain = 0, st_steps = 0, st_pieces = 0, st_t1 = 0;
+#endif
   if ((int)blockIdx.x < P.njobs) {                         // ---- a chain
     const int j = blockIdx.x;
     for (int s = P.job_seg0[j]; s < P.job_seg0[j + 1]; ++s) {
@@ -358,6 +368,10 @@ __global__ void __launch_bounds__(256) k_br_persist(BrPersistArgs P) {
       for (int64_t a = JS.u0, c = 0; a < JS.u1; a += P.chunk, ++c) {
         const int64_t b = a + P.chunk < JS.u1 ? a + P.chunk : JS.u1;
         if (threadIdx.x == 0) {                            // the iteration's one thread-0 region
+#ifdef NFSP_BRP_STAMPS
+          const unsigned long long t0 = BRP_T();
+          if (st_t1) st_chain += t0 - st_t1;
+#endif
           const uint32_t* done = &P.chunk_done[P.seg_chunk0[s] + c];
           int it = 0;
           while (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)(b - a) &&
@@ -366,6 +380,12 @@ __global__ void __launch_bounds__(256) k_br_persist(BrPersistArgs P) {
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
           s_word = it >= P.spin;
           if (s_word) brp_bail(P.err, 1);
+#ifdef NFSP_BRP_STAMPS
+          st_t1 = BRP_T();
+          st_wait += st_t1 - t0;
+          st_steps += (b - a) * P.C.E * (P.C.B / CHAIN_MB);
+          ++st_pieces;
+#endif
         }
         __syncthreads();
         if (s_word) return;                                // workgroup-uniform
@@ -388,11 +408,22 @@ __global__ void __launch_bounds__(256) k_br_persist(BrPersistArgs P) {
         __syncthreads();        // s_word is rewritten by the next wait
       }
     }
+#ifdef NFSP_BRP_STAMPS
+    if (threadIdx.x == 0) {
+      if (st_t1) st_chain += BRP_T() - st_t1;
+      unsigned long long* d = g_brp_stamps[0][j & 63];
+      atomicAdd(d + 0, st_wait); atomicAdd(d + 1, st_chain); atomicAdd(d + 2, st_steps); atomicAdd(d + 3, st_pieces);
+    }
+#endif
     return;
   }
   uint32_t* prev_done = nullptr;                           // thread 0: the last item's chunk counter
   for (;;) {                                                // ---- a helper
     if (threadIdx.x == 0) {                                // the iteration's one thread-0 region:
+#ifdef NFSP_BRP_STAMPS
+      const unsigned long long t0 = BRP_T();
+      if (st_t1) st_chain += t0 - st_t1;                   // (helpers: work cycles)
+#endif
       if (prev_done)                                       // publish the last item, take the next
         __hip_atomic_fetch_add(prev_done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       const uint32_t p = __hip_atomic_fetch_add(&P.ctr[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -409,6 +440,15 @@ __global__ void __launch_bounds__(256) k_br_persist(BrPersistArgs P) {
         }
       }
       s_word = v;
+#ifdef NFSP_BRP_STAMPS
+      st_t1 = BRP_T();
+      st_wait += st_t1 - t0;
+      if (v != BRP_DONE) ++st_steps;
+      if (v == BRP_DONE) {
+        unsigned long long* d = g_brp_stamps[1][(blockIdx.x - P.njobs) & 63];
+        atomicAdd(d + 0, st_wait); atomicAdd(d + 1, st_chain); atomicAdd(d + 2, st_steps);
+      }
+#endif
     }
     __syncthreads();
     const uint32_t v = s_word;
@@ -1691,6 +1731,18 @@ extern "C" int nfsp_group_get_sched(nfsp_group* g, nfsp_group_sched* out) {
   *out = g->sched;
   return NFSP_OK;
 }
+
+#ifdef NFSP_BRP_STAMPS
+extern "C" int nfsp_debug_brp_stamps(unsigned long long* out, int reset) {
+  NFSP_HIP(hipDeviceSynchronize());
+  NFSP_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_brp_stamps), sizeof(g_brp_stamps)));
+  if (reset) {
+    static unsigned long long zero[2][64][4] = {};
+    NFSP_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_brp_stamps), zero, sizeof(zero)));
+  }
+  return NFSP_OK;
+}
+#endif
 
 extern "C" int nfsp_group_check(nfsp_group* g) {
   NFSP_REQUIRE(g, "null argument");
