@@ -1,10 +1,11 @@
 #!/bin/bash
 # Build the chain microbenchmark (tools/bench_chain.hip) with the engine's chain flags:
 #   tools/build_chain_bench.sh <tag> [extra hipcc flags]  ->  tools/bin/bench_chain_<tag>_{ar,br}
+# (SCHED=<strategy> replaces the machine scheduler strategy, default max-ilp)
 set -e
 tag=${1:?tag}; shift
 PKG=neural-ficititious-self-play-in-imperfect-information-games_amd
-F="--offload-arch=gfx950 -O3 -std=c++17 -mllvm -amdgpu-mfma-vgpr-form -fno-slp-vectorize -fno-honor-nans -falign-loops=64 -mllvm -amdgpu-sched-strategy=max-ilp -Iinclude -I$PKG/csrc"
+F="--offload-arch=gfx950 -O3 -std=c++17 -mllvm -amdgpu-mfma-vgpr-form -fno-slp-vectorize -fno-honor-nans -falign-loops=64 -mllvm -amdgpu-sched-strategy=${SCHED:-max-ilp} -Iinclude -I$PKG/csrc"
 mkdir -p tools/bin
 hipcc $F "$@" tools/bench_chain.hip -o tools/bin/bench_chain_${tag}_ar
 hipcc $F "$@" tools/bench_chain.hip -o tools/bin/bench_chain_${tag}_br
