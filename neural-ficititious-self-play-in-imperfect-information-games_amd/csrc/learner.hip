@@ -339,8 +339,10 @@ struct BrPersistArgs {
 constexpr uint32_t BRP_EMPTY = 0xFFFFFFFFu, BRP_DONE = 0xFFFFFFFEu;
 constexpr int BRP_SPIN = 1 << 18;           // x s_sleep 8 (~56 ms): far past any legitimate wait
 constexpr int BRP_CHUNK = 16;               // updates per chain piece (readiness is checked per piece)
-constexpr int BRP_HELPERS = 48;             // helper workgroups (c4_emul_r8: 96 / 160 took the
-                                            // step 217.7 -> 207.2 / 205.2 ms; the rounds 179.6)
+constexpr int BRP_HELPERS = 48;             // helper workgroups (c4_emul_r8, timeline tool, with
+                                            // the scalar jobs: 96 / 144 / 192 helpers 193.1 /
+                                            // 189.5 / 188.1 ms, the AR chains slowing 155 -> 166;
+                                            // the rounds 179.6)
 constexpr int BRP_STATIC_LDS = 16 * 1024;   // bound on the kernel's static LDS (the targets buffers)
 
 #ifdef NFSP_BRP_STAMPS
@@ -349,6 +351,28 @@ constexpr int BRP_STATIC_LDS = 16 * 1024;   // bound on the kernel's static LDS 
 __device__ unsigned long long g_brp_stamps[2][64][4];
 #define BRP_T() __builtin_amdgcn_s_memtime()
 #endif
+
+// A job read from the tables arrives in VGPRs (vector loads: the kernel writes global memory,
+// so no scalar loads); readfirstlane makes its fields scalar again, as k_chain3's kernel-argument
+// jobs are -- otherwise every record load's buffer descriptor becomes a readfirstlane loop
+__device__ __forceinline__ int64_t brp_u64(int64_t x) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+template <class T>
+__device__ __forceinline__ T* brp_ptr(T* p) { return reinterpret_cast<T*>(brp_u64(reinterpret_cast<int64_t>(p))); }
+__device__ __forceinline__ ChainJob brp_uniform(ChainJob J) {
+  J.w = brp_ptr(J.w);
+  J.sync_to = brp_ptr(J.sync_to);
+  J.snap_to = brp_ptr(J.snap_to);
+  J.rec = brp_ptr(J.rec);
+  J.active = brp_ptr(J.active);
+  J.loss_out = brp_ptr(J.loss_out);
+  J.u0 = brp_u64(J.u0);
+  J.u1 = brp_u64(J.u1);
+  return J;
+}
 
 __device__ __forceinline__ void brp_bail(int32_t* err, int k) {
   __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -364,7 +388,7 @@ __global__ void __launch_bounds__(256) k_br_persist(BrPersistArgs P) {
   if ((int)blockIdx.x < P.njobs) {                         // ---- a chain
     const int j = blockIdx.x;
     for (int s = P.job_seg0[j]; s < P.job_seg0[j + 1]; ++s) {
-      const ChainJob JS = P.seg_job[s];
+      const ChainJob JS = brp_uniform(P.seg_job[s]);
       for (int64_t a = JS.u0, c = 0; a < JS.u1; a += P.chunk, ++c) {
         const int64_t b = a + P.chunk < JS.u1 ? a + P.chunk : JS.u1;
         if (threadIdx.x == 0) {                            // the iteration's one thread-0 region
@@ -388,7 +412,11 @@ __global__ void __launch_bounds__(256) k_br_persist(BrPersistArgs P) {
 #endif
         }
         __syncthreads();
-        if (s_word) return;                                // workgroup-uniform
+        // readfirstlane: the compiler then knows the value is uniform -- a scalar branch, a loop
+        // with uniform exits (with a vector value the loop's exits are divergent, values carried
+        // in it are taken as divergent and every record load's buffer descriptor became a
+        // readfirstlane loop: 1,280 instructions per 4 steps against k_chain3's 1,217)
+        if (__builtin_amdgcn_readfirstlane(s_word)) return; // workgroup-uniform
         ChainJob JP = JS;
         JP.u0 = a;
         JP.u1 = b;
@@ -401,7 +429,7 @@ __global__ void __launch_bounds__(256) k_br_persist(BrPersistArgs P) {
         const uint32_t m = (uint32_t)P.seg_tgt[s + 1].n;
         if (threadIdx.x == 0) s_word = __hip_atomic_fetch_add(&P.ctr[1], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
-        const uint32_t base = s_word;
+        const uint32_t base = __builtin_amdgcn_readfirstlane(s_word);
         for (uint32_t i = threadIdx.x; i < m; i += blockDim.x)
           __hip_atomic_store(&P.slots[base + i], ((uint32_t)(s + 1) << 16) | i, __ATOMIC_RELEASE,
                              __HIP_MEMORY_SCOPE_AGENT);
@@ -451,9 +479,9 @@ __global__ void __launch_bounds__(256) k_br_persist(BrPersistArgs P) {
 #endif
     }
     __syncthreads();
-    const uint32_t v = s_word;
+    const uint32_t v = __builtin_amdgcn_readfirstlane(s_word);
     __syncthreads();
-    if (v == BRP_DONE) return;                             // workgroup-uniform
+    if (v == BRP_DONE) return;                             // workgroup-uniform (scalar)
     const int s = (int)(v >> 16);
     const int64_t i = (int64_t)(v & 0xFFFFu);
     br_targets_item(P.seg_tgt[s], i, P.C.B, P.C.E, P.gamma, P.quirks, P.lr0);
