@@ -8,6 +8,8 @@ The standalone engine is itself pinned to the oracle (test_gpu_engine / test_gpu
 so this carries that parity over to the grouped launches.  With the AR exchange on, the AR
 nets equal shards.AvgPolicyAllReduce's W0 + sum_r (W_r - W0) / R, recomputed here in numpy
 f32 in replica order from standalone engines stepped from the same common nets."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -46,7 +48,7 @@ def test_group_replicas_match_standalone_engines(pkg, quirks, R):
         for e in solo:
             e.step()
         torch.cuda.synchronize()
-        assert g.rounds() >= 2
+        assert g.rounds() >= 2 or g.sched()["br_persist"]   # (one launch under NFSP_GROUP_BR_PERSIST)
         for r in range(R):
             a_st, b_st = g.replicas[r].stats(), solo[r].stats()
             for k in STAT_KEYS:
@@ -222,13 +224,15 @@ def test_group_sched_changes_no_sgd_step(pkg):
     pieces on 4 partitions, and the serial slice loop: nets and counters bit for bit the same
     (a piece resumes from the weights in memory; the partitions run the same pieces)."""
     kw = dict(n_lanes=65_536, slices=16, slice_lag=2, rl_capacity=200_000, sl_capacity=400_000)
-    variants = [None, dict(br_cap=0, br_pace=0, br_streams=1), dict(br_cap=16, br_pace=0, br_streams=4),
-                dict(br_cap=40, br_pace=1, br_streams=3), dict(serial=1), dict(br_persist=1)]
+    variants = [dict(br_persist=0), dict(br_cap=0, br_pace=0, br_streams=1, br_persist=0),
+                dict(br_cap=16, br_pace=0, br_streams=4, br_persist=0),
+                dict(br_cap=40, br_pace=1, br_streams=3, br_persist=0), dict(serial=1), dict(br_persist=1)]
     runs = []
     for v in variants:
         g = pkg.engine.EngineGroup(4, seed=5151, init_seed=4, **kw)
         d = g.sched()
-        assert d == dict(br_cap=-1, br_pace=1, br_streams=-1, serial=0, br_persist=0), d
+        if not any(k.startswith("NFSP_GROUP_") for k in os.environ):   # the defaults' environment
+            assert d == dict(br_cap=-1, br_pace=1, br_streams=-1, serial=0, br_persist=0), d
         if v:
             g.set_sched(**v)
             assert all(g.sched()[k] == x for k, x in v.items())
