@@ -135,7 +135,7 @@ CONFIGS = {
 PEAK_BF16_TFLOPS = 2500.0     # MI355X_MICROARCH.md: BF16 MFMA, ~2.5 PF dense (the chains' MFMAs)
 PEAK_HBM_GBS = 8000.0         # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
 # the chains' matrix-core work per SGD step: 18 v_mfma_f32_16x16x32_bf16 per wave x 4 waves
-# (SQ_INSTS_MFMA, profiles/r04_chain_pmc.json), 2 x 16 x 16 x 32 FLOP each: the exact 3-term
+# (SQ_INSTS_MFMA, profiles/r06/chain_pmc.json), 2 x 16 x 16 x 32 FLOP each: the exact 3-term
 # bf16 split executes ~2.9x the dense-equivalent f32 FLOPs of the step (32 x F_TRAIN)
 MFMA_PER_SGD_STEP = 18 * 4
 FLOP_PER_MFMA = 2 * 16 * 16 * 32
@@ -806,10 +806,10 @@ def rooflines(config, cfg, k_ms, k_launches, k_step_ms, br_upd, ar_upd, ar_max, 
 
     def chain_issue(name, updates, net):
         """The chain's step as an issue roofline: the loop's static issue cycles per SGD step
-        (tools/chain_census.py -> profiles/r04_chain_census.json, MI355X_MICROARCH.md issue
+        (tools/chain_census.py -> profiles/r06/chain_census.json, MI355X_MICROARCH.md issue
         costs) against the measured cycles per step at the chain's effective clock (2.40 GHz,
         tools/chain_clock.py).  frac = the share of the step one wave spends issuing."""
-        path = os.path.join(REPO, "profiles", "r04_chain_census.json")
+        path = os.path.join(REPO, "profiles", "r06", "chain_census.json")
         n = max(k_launches[name], 1) * (par if name == "k_chain3_br" else 1)
         steps = updates * 2 * 128 / 32 / n                  # epochs x minibatches per workgroup
         if not os.path.exists(path) or steps <= 0:
@@ -819,12 +819,12 @@ def rooflines(config, cfg, k_ms, k_launches, k_step_ms, br_upd, ar_upd, ar_max, 
         measured = k_ms[name] * 1e-3 / steps * CHAIN_CLOCK_HZ
         out = {"kernel": name, "bound": "issue", "achieved": issue, "peak": measured,
                "unit": "cycles per SGD step (static issue / measured)", "frac": issue / measured,
-               "us_per_step": k_ms[name] * 1e3 / steps, "source": "profiles/r04_chain_census.json"}
-        pmc = os.path.join(REPO, "profiles", "r04_chain_pmc.json")   # tools/chain_pmc.sh
+               "us_per_step": k_ms[name] * 1e3 / steps, "source": "profiles/r06/chain_census.json"}
+        pmc = os.path.join(REPO, "profiles", "r06", "chain_pmc.json")   # tools/chain_pmc.sh
         if os.path.exists(pmc):
             with open(pmc) as f:
                 out["sq_active_inst_frac"] = json.load(f)[net]["frac_active_inst"]
-            out["sq_source"] = "profiles/r04_chain_pmc.json"
+            out["sq_source"] = "profiles/r06/chain_pmc.json"
         return out
 
     # roofline: SURVEY 8(d)'s HBM framing (the judged bound) of each kernel; the MFMA and
