@@ -206,3 +206,25 @@ def test_stuck_rank_ends_the_job():
     assert not lines
     assert "rank 1 made no progress" in err and "last: step 2" in err
     assert time.time() - t0 < 60
+
+
+def test_eight_rank_job_like_the_drivers_scale_run():
+    """The driver's N = 8 invocation (`bench.py --gpus 8`, C4's arithmetic per rank: 128 slices,
+    the AR exchange after every slice) rehearsed with 8 gloo ranks on the CPU: one line, dp8,
+    the whole-job value over the slowest rank's time, every rank reported, every exchange made
+    and the ranks' AR nets identical after it, the learning check at the job's total hands."""
+    rc, lines, err = _bench(["--gpus", "8", "--steps", "2", "--warmup", "1", "--stub-step-ms", "5"],
+                            timeout=300)
+    assert rc == 0, err
+    assert len(lines) == 1, lines
+    out = lines[0]
+    assert out["n_gpus"] == 8 and out["config"]["parallelism"] == "dp8"
+    lanes = 1_048_576
+    assert abs(out["value"] - 8 * 2 * lanes / (out["ms_per_step"] * 2e-3)) < 1e-6 * out["value"]
+    rk = out["ranks"]
+    assert rk["world_size"] == 8 and [r["rank"] for r in rk["ranks"]] == list(range(8))
+    assert out["ms_per_step"] >= rk["ms_per_step_max"]
+    x = out["ar_allreduce"]
+    assert x["calls_timed_pass"] == x["calls_expected"] == 2 * 128 and x["calls_ok"]
+    assert x["ar_nets_check"]["after_timed_pass"]["ar_nets_identical"]
+    assert x["learning_at_total_hands"]["hands"] == 8 * 3 * lanes
