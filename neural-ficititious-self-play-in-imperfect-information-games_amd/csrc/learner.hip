@@ -320,6 +320,8 @@ __device__ __forceinline__ void br_targets_item(const TargetJob J, int64_t bx, i
 // own, which left the barrier-bearing body as an inner loop that lanes 1-63 of wave 0 and waves
 // 1-3 iterated on the stale work word while lane 0 waited for them to leave it: the hang of
 // profiles/r05_group_br_persist (found in round 6 in the ISA, profiles/r06/persist_rootcause).
+// The words that end the loops (a bail, the next item) are read through readfirstlane, so the
+// loops' exits are scalar branches, and a job's fields are made scalar (brp_uniform).
 // ---------------------------------------------------------------------------
 struct BrPersistArgs {
   ChainArgs C;                  // B, E (the chains' jobs come from seg_job)
