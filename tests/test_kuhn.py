@@ -252,3 +252,29 @@ def test_gpu_kuhn_c5_exploitability_below_0_05(pkg):
         eng.step()
     e1 = eng.exploitability(0)["exploitability"]
     assert e0 > 1.0 and e1 < 0.05, (e0, e1)
+
+
+@pytest.mark.parametrize("p", [0.55, 0.7])
+def test_huber_q_fixed_point_is_not_the_mean(p):
+    """Reason of record for the reference algorithm's Kuhn plateau.  Its BR loss
+    is Huber (agent/agent.py:91-99): the gradient clamp(e, -1, 1) drives a Q value whose target
+    is a +-2-chip showdown won with probability p to the point where E clamp(t - q) = 0, i.e.
+    q = 2 - (1 - p) / p for p > 1/2 -- not the mean 4p - 2.  At p = 0.55 that is 1.18 against
+    0.2: Q jumps by ~2 chips around p = 1/2, where fictitious play keeps the opponent's mixing.
+    The MSE form (NFSP_EXT_MSE_Q) converges to the mean.  The oracle's Keras restatement
+    (nn_oracle.MLP, linear head so no unit dies), one observation, the reference's fit."""
+    obs = np.zeros((1, nn.N_IN), np.float32)
+    obs[0, [0, 13, 24]] = 1.0                     # a history bit, another, a card
+    out = {}
+    for act in (nn.ACT_LINEAR, nn.ACT_LINEAR_MSE):
+        net = nn.MLP(act, rng=np.random.RandomState(3))
+        rng = np.random.RandomState(11)
+        tail = []
+        for u in range(600):
+            t = np.where(rng.random_sample((128, 1)) < p, 2.0, -2.0).astype(np.float32) * np.ones((1, 3), np.float32)
+            net.fit(np.repeat(obs, 128, axis=0), t, 0.02, shuffle_rng=rng)
+            if u >= 400:
+                tail.append(float(net.predict(obs)[0].mean()))
+        out[act] = float(np.mean(tail))
+    assert abs(out[nn.ACT_LINEAR] - (2 - (1 - p) / p)) < 0.1, out
+    assert abs(out[nn.ACT_LINEAR_MSE] - (4 * p - 2)) < 0.1, out
