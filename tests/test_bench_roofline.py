@@ -152,3 +152,13 @@ def test_r06_line_frac_matches_rocprof_within_one_percent():
     avg_ms = float(rows[0]["AverageNs"]) * 1e-6
     frac_rocprof = roof["bytes_per_launch"] / (avg_ms * 1e-3) / 1e9 / roof["peak"]
     assert abs(frac_rocprof - roof["frac"]) <= 0.01 * roof["frac"], (frac_rocprof, roof["frac"])
+
+
+def test_persist_group_line_is_c4_emul_r8_with_one_setting():
+    """bench.CONFIGS['c4_emul_r8_persist'] differs from c4_emul_r8 only in the schedule
+    (br_persist) and its label: the two lines compare one setting."""
+    import bench
+    a, b = dict(bench.CONFIGS["c4_emul_r8"]), dict(bench.CONFIGS["c4_emul_r8_persist"])
+    assert b.pop("sched") == {"br_persist": 1}
+    a.pop("label"), b.pop("label")
+    assert a == b
